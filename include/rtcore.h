@@ -1,0 +1,236 @@
+/*
+ * rtcore.h — C ABI of the MI355X-native renderer core (libmyrt.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel trace path
+ * (erndmrcn/MyRayTracer).  A host (the Swift `RayTracerEngine`, or the Python
+ * mirror in myraytracer_amd/engine.py) describes a scene with plain C structs,
+ * creates a device-resident scene once, and renders cameras from it.
+ *
+ * Each entry point cites the reference interface it replaces
+ * (paths relative to Sources/ of the reference):
+ *
+ *   rt_scene_create   <- RayTracerEngine.init(from:data:)  RayTracer/RayTracer.swift:30-49
+ *                        + RTContext.init(scene:)         RayTracer/Models/RTContext.swift:94-418
+ *   rt_render         <- RayTracerEngine.render(format:cameraIndex:progress:)
+ *                                                          RayTracer/RayTracer.swift:115-131
+ *                        -> renderRGBA8Async               RayTracer/RayTracer.swift:137-205
+ *                        -> Renderer.render(scene:cameraIndex:progressRow:)
+ *                                                          RayTracer/Extensions/Object+Extension.swift:52-379
+ *   rt_render_device  <- same path, output left in device memory (bench / multi-GPU)
+ *   rt_scene_info     <- RayTracerEngine.inspect / sceneMeshAndTriangleCounts
+ *                                                          RayTracer/RayTracer.swift:52-67,208-227
+ *   rt_ply_load       <- PLYLoader.load(from:)             RayTracer/Helpers/PLYReader.swift:54-210
+ *                        (which drives CPly's ply_reader_* C ABI, CPly/include/PLYReaderWrapper.h:26-69)
+ *
+ * Conventions mirror the reference's only C ABI (CPly/include/PLYReaderWrapper.h:22-69,
+ * CPly/wrapper.cpp:17-27): opaque handle + create/destroy pair, caller-allocated
+ * outputs, no C++ exception ever crosses the boundary.  Status codes: 0 = OK,
+ * negative = error; the reference's NSError codes are reused (-10, -20, -21,
+ * RayTracer.swift:121,141-154).  rt_last_error() returns a thread-local message.
+ *
+ * All arithmetic is IEEE binary64 (the reference's Vec3 = SIMD3<Double>,
+ * RTContext.swift:13-16).  Matrices are column-major 4x4 (simd_double4x4 layout:
+ * m[c*4 + r] = column c, row r).
+ */
+#ifndef MYRT_RTCORE_H
+#define MYRT_RTCORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define RT_OK                    0
+#define RT_ERR_INVALID_CAMERA  (-10)  /* RayTracer.swift:151-154 "Invalid camera index" */
+#define RT_ERR_NO_SCENE        (-20)  /* RayTracer.swift:141-144 "No scene loaded"      */
+#define RT_ERR_NO_RENDERER     (-21)  /* RayTracer.swift:145-148 "Renderer not initialized" */
+#define RT_ERR_INVALID_ARG     (-30)
+#define RT_ERR_UNSUPPORTED     (-31)  /* feature outside the implemented hot path      */
+#define RT_ERR_PLY             (-40)  /* PLYReader.swift:24-40 PlyError                */
+#define RT_ERR_DEVICE          (-50)  /* HIP runtime failure                           */
+#define RT_ERR_OOM             (-51)
+#define RT_ERR_CANCELLED       (-60)  /* progress callback returned 0                  */
+#define RT_ERR_STACK           (-61)  /* BVH deeper than the traversal stack           */
+
+/* ---- scene description (ParsingKit Scene stand-in) ----------------------- */
+typedef struct rt_vec3 { double x, y, z; } rt_vec3;
+
+/* Material.type strings of the reference (Object+Extension.swift:189,207,252) */
+#define RT_MAT_DEFAULT     0
+#define RT_MAT_MIRROR      1   /* "mirror"     */
+#define RT_MAT_DIELECTRIC  2   /* "dielectric" */
+#define RT_MAT_CONDUCTOR   3   /* "conductor"  */
+
+typedef struct rt_material {   /* ParsingKit Material, fields read in trace() */
+    rt_vec3 ambient, diffuse, specular, mirror, absorption;
+    double  phong;              /* Phong exponent, clamped to >= 1 (:131)      */
+    double  ior;                /* refraction index; > 0 disables direct light on back faces (:112-115) */
+    double  absorption_index;   /* conductor k (:254)                           */
+    double  roughness;          /* glossy perturbation (:191-197)               */
+    int32_t type;               /* RT_MAT_*                                     */
+    int32_t _pad;
+} rt_material;
+
+typedef struct rt_point_light { rt_vec3 position, intensity; } rt_point_light;
+
+typedef struct rt_area_light {  /* Object+Extension.swift:145-186 */
+    rt_vec3 position, normal, radiance;
+    double  size;
+} rt_area_light;
+
+#define RT_CAM_LOOKAT     0     /* cam.type == "lookAt" (Object+Extension.swift:394)   */
+#define RT_CAM_NEARPLANE  1     /* explicit nearPlane + gaze (:415-426)                */
+
+typedef struct rt_camera {      /* ParsingKit Camera */
+    int32_t type;               /* RT_CAM_*                                            */
+    int32_t width, height;      /* imageResolution                                     */
+    int32_t num_samples;        /* numSamples                                          */
+    rt_vec3 position, gaze_point, gaze, up;
+    double  fovy;               /* degrees; NaN = absent (Camera.fovy: Double?)        */
+    double  near_distance;
+    double  near_plane[4];      /* l, r, b, t                                          */
+    double  aperture_size, focus_distance;
+} rt_camera;
+
+#define RT_OBJ_MESH           0
+#define RT_OBJ_TRIANGLE       1
+#define RT_OBJ_SPHERE         2
+#define RT_OBJ_PLANE          3
+#define RT_OBJ_MESH_INSTANCE  4
+
+/* One entry of Scene.objects, in scene order (RTContext.swift:120-378). */
+typedef struct rt_object {
+    int32_t kind;               /* RT_OBJ_*                                            */
+    int32_t material_id;        /* materialIndex(for:) = Int(id) or -1 (RTContext.swift:423-426), 1-based */
+    int32_t smooth;             /* Mesh.shadingMode == "smooth" (RTContext.swift:245)  */
+    int32_t id;                 /* object id (MeshInstance.baseMeshID refers to it)    */
+    int32_t base_mesh_id;       /* RT_OBJ_MESH_INSTANCE only                           */
+    int32_t indices_one_based;  /* inline faces.data are 1-based (RTContext.swift:300-301) */
+    double  transform[16];      /* composed localToWorld (Scene.composeTransform result), column-major */
+    rt_vec3 motion_blur;        /* Mesh.motionBlur / MeshInstance.motionBlur           */
+    /* mesh payload: either a PLY path or inline arrays                               */
+    const char*    ply_path;
+    const double*  positions;   int64_t num_positions;   /* xyz triples               */
+    const int32_t* indices;     int64_t num_indices;     /* triangle list             */
+    const double*  normals;     /* optional per-vertex normals (PLY branch, RTContext.swift:267-297) */
+    /* analytic payloads (RT_OBJ_TRIANGLE / SPHERE / PLANE)                           */
+    rt_vec3 v[3];               /* triangle vertices                                   */
+    rt_vec3 center;             /* sphere / plane center                               */
+    rt_vec3 normal;             /* plane normal                                        */
+    double  radius;             /* sphere radius                                       */
+} rt_object;
+
+typedef struct rt_scene_desc {
+    rt_vec3 background_color;
+    rt_vec3 ambient_light;             /* scene.lights.ambient                         */
+    double  shadow_ray_epsilon;
+    double  intersection_test_epsilon;
+    int32_t max_recursion_depth;
+    int32_t num_materials;
+    const rt_material*    materials;
+    int32_t num_point_lights;
+    int32_t num_area_lights;
+    const rt_point_light* point_lights;
+    const rt_area_light*  area_lights;
+    int32_t num_objects;
+    int32_t num_cameras;
+    const rt_object*      objects;
+    const rt_camera*      cameras;
+} rt_scene_desc;
+
+/* ---- results -------------------------------------------------------------- */
+typedef struct rt_stats {       /* RenderStats (Models/RenderStats.swift:8-24) + ray counts */
+    int64_t meshes, triangles, spheres, planes;
+    int64_t primary_rays;       /* W*H*n^2 actually cast                               */
+    int64_t shadow_rays;        /* one per point light per directly-lit hit            */
+    int64_t secondary_rays;     /* reflection rays                                     */
+    double  milliseconds;       /* wall time of the render call                        */
+    double  kernel_ms;          /* device time of the render kernels                   */
+} rt_stats;
+
+typedef struct rt_scene_info {
+    int64_t meshes, triangles, spheres, planes, instances;
+    int64_t blas_nodes, tlas_nodes, max_depth;
+    double  build_ms;           /* PLY load + flatten + BVH build + layout            */
+    double  upload_ms;          /* host -> device copies                               */
+    int64_t device_bytes;       /* per-device resident scene bytes                     */
+} rt_scene_info;
+
+typedef struct rt_scene rt_scene;   /* opaque */
+
+/* progress: rows finished so far; return 0 to cancel (RayTracer.swift:172-181). */
+typedef int (*rt_progress_fn)(void* user, int32_t rows_done, int32_t rows_total);
+
+/* ---- lifecycle ------------------------------------------------------------- */
+/* Builds the scene on the host (PLY load, flattening, SAH BVH) and uploads a full
+ * replica to each listed device (HIP ordinals; n_devices <= 0 means device 0). */
+int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32_t n_devices,
+                        rt_scene** out);
+void    rt_scene_destroy(rt_scene* scene);
+int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
+
+/* ---- rendering -------------------------------------------------------------- */
+/* Renders 8-row chunks chunk_first, chunk_first+chunk_step, ... of camera
+ * `camera_index` (chunk c covers rows [8c, min(8c+8, H)) as in
+ * Object+Extension.swift:75-82; row 0 = top).  Outputs are caller-owned HOST
+ * buffers holding the selected chunks' rows packed in chunk order:
+ * out_rgb = rows*W*3 doubles (the [Vec3] of Renderer.render), out_rgba8 =
+ * rows*W*4 bytes (RayTracer.swift:186-195).  Either may be NULL.  chunk_step = 1,
+ * chunk_first = 0 renders the whole image.  Work is spread over all devices of
+ * the scene. */
+int32_t rt_render(rt_scene* scene, int32_t camera_index, int32_t chunk_first, int32_t chunk_step,
+                  double* out_rgb, uint8_t* out_rgba8, rt_stats* stats,
+                  rt_progress_fn progress, void* user);
+
+/* Same as rt_render on ONE device slot, but outputs are DEVICE pointers on that
+ * device and the work is enqueued on `stream` (a hipStream_t, NULL = default)
+ * without host synchronisation.  Ray counters (if stats != NULL) are only valid
+ * after rt_stats_collect() once the stream has drained. */
+int32_t rt_render_device(rt_scene* scene, int32_t device_slot, int32_t camera_index,
+                         int32_t chunk_first, int32_t chunk_step,
+                         double* d_out_rgb, uint8_t* d_out_rgba8, void* stream);
+int32_t rt_stats_collect(rt_scene* scene, int32_t device_slot, rt_stats* stats);
+
+/* Number of output rows rt_render writes for a chunk selection. */
+int32_t rt_rows_for_chunks(int32_t height, int32_t chunk_first, int32_t chunk_step);
+
+/* Traversal work counters of the last rt_render_device on a slot (instrumented
+ * kernel variant; used to price algorithmic bytes for the roofline). */
+typedef struct rt_work_counters {
+    int64_t records_fetched;    /* 128-B two-child node records loaded                */
+    int64_t tri_tests;          /* 80-B triangle records tested                       */
+    int64_t normal_fetches;     /* 72-B smooth-normal triples loaded (final hits)     */
+    int64_t instance_entries;   /* world->local transforms                            */
+    int64_t pixels;             /* pixels written                                     */
+} rt_work_counters;
+int32_t rt_render_device_counted(rt_scene* scene, int32_t device_slot, int32_t camera_index,
+                                 int32_t chunk_first, int32_t chunk_step,
+                                 double* d_out_rgb, void* stream, rt_work_counters* out);
+
+const char* rt_last_error(void);
+const char* rt_version(void);
+
+/* ---- PLY (host) --------------------------------------------------------------- */
+typedef struct rt_ply_mesh {            /* PlyMesh (PLYReader.swift:14-19)           */
+    double*  positions;  int64_t num_positions;   /* float32 widened to double (:96-102) */
+    double*  normals;    int64_t num_normals;     /* normalized (:105-123), 0 if absent  */
+    float*   texcoords;  int64_t num_texcoords;
+    int32_t* indices;    int64_t num_indices;     /* triangulated, 0-based (:149-198)    */
+} rt_ply_mesh;
+int32_t rt_ply_load(const char* path, rt_ply_mesh* out);
+void    rt_ply_free(rt_ply_mesh* mesh);
+
+/* ---- debug / test hooks (not part of the reference surface) -------------------- */
+/* Canonical hash of instance `instance`'s BLAS (instance = -1: the TLAS); equal to the
+ * oracle's oracle_bvh_hash when the topology, bounds and leaf order match BVH.swift. */
+uint64_t rt_debug_bvh_hash(const rt_scene* scene, int32_t instance);
+/* Host-only build (no device): hashes[0..n) per instance, hashes[n] = TLAS. */
+int32_t  rt_debug_host_build(const rt_scene_desc* desc, uint64_t* hashes, int32_t max_hashes,
+                             int32_t* n_instances, rt_scene_info* info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MYRT_RTCORE_H */

@@ -1,0 +1,100 @@
+// layout.h — device-resident scene layout shared by the host builder (scene.cpp)
+// and the HIP kernels (render.hip).  Everything is IEEE binary64 like the
+// reference (RTContext.swift:13-16).
+//
+// HBM layout (per device replica):
+//   recs    : WRec[]    128-B two-child BVH records, one per INNER node of every
+//             BLAS and of the TLAS (RT/Accelearion/BVH.swift:16-30 nodes, re-laid so
+//             that a parent holds both children's bounds -> one cache line per
+//             visited inner node instead of two 56-B node reads + a re-test).
+//   tris    : TriRec[]  80-B {v0, e1, e2, last-in-leaf} in BVH LEAF order, so a leaf
+//             is a contiguous run (removes primIdx -> prims -> triangles indirection,
+//             RTContext.swift:573-581).
+//   normals : double[9] per TriRec (n0, n1, n2), read only for the final hit.
+//   insts   : DInstance[] (RTContext.swift:43-61) + TLAS leaf instance lists.
+#pragma once
+#include <stdint.h>
+
+namespace myrt {
+
+// Child reference encoding used in WRec.ref[], stack entries and instance roots:
+//   ref >= 0 : inner node -> index of its WRec
+//   ref <  0 : leaf       -> ~ref = index of its first TriRec (BLAS) or first
+//                            TLAS leaf-list entry; the run ends at the entry whose
+//                            `last` flag is set.
+struct alignas(128) WRec {
+    double lo[2][3];      // child c aabbMin (x,y,z)
+    double hi[2][3];      // child c aabbMax
+    int32_t ref[2];       // child refs (c = 0 is the reference's L = leftFirst, c = 1 is R)
+    int32_t pad[6];
+};
+static_assert(sizeof(WRec) == 128, "WRec must be one 128-B line");
+
+struct alignas(16) TriRec {
+    double v0[3], e1[3], e2[3];
+    int32_t last;         // 1 = last triangle of its leaf
+    int32_t prim;         // original triangle index (reference `triangles[]` order)
+};
+static_assert(sizeof(TriRec) == 80, "TriRec is 80 B");
+
+struct DMaterial {        // ParsingKit Material fields used by trace()
+    double ambient[3], diffuse[3], specular[3], mirror[3], absorption[3];
+    double phong, ior, absorption_index, roughness;
+    int32_t type, pad;
+};
+
+struct DPointLight { double position[3], intensity[3]; };
+
+struct DInstance {        // Instance (RTContext.swift:43-61) + its BLAS entry point
+    double w2l[16];       // worldToLocal, column-major
+    double l2w[16];       // localToWorld
+    double nmat[9];       // normalMatrix = inverse(M3)^T, column-major
+    double motion[3];     // instanceMotion
+    double tri_motion[3]; // Triangle.motionBlur of the mesh (uniform per BLAS)
+    double root_lo[3], root_hi[3];   // BLAS root node bounds (tested first, RTContext.swift:567-571)
+    int32_t root_ref;     // BLAS root ref (global)
+    int32_t material;     // materialOverride (always set by makeInstance callers)
+    int32_t smooth;       // prim shadingMode == .smooth
+    int32_t det_neg;      // simd_determinant(M3) < 0
+};
+
+struct DTlasLeafEntry { int32_t inst; int32_t last; };
+
+// Camera + frame constants precomputed on the host (Object+Extension.swift:58-93)
+struct DCamera {
+    double eye[3], u[3], v[3], w[3];
+    double q00[3];
+    double du, dv, nd;
+    double aperture, focus;
+    int32_t width, height, samples, n;   // samples = max(1, numSamples); n = Int(sqrt(samples))
+};
+
+struct RenderParams {
+    const WRec* recs;
+    const TriRec* tris;
+    const double* normals;
+    const DInstance* insts;
+    const DTlasLeafEntry* tlas_leaf;
+    const DMaterial* mats;
+    const DPointLight* plights;
+    double tlas_root_lo[3], tlas_root_hi[3];
+    int32_t tlas_root_ref;
+    int32_t has_tlas;
+    int32_t num_mats;
+    int32_t num_plights;
+    DCamera cam;
+    double eps, shadow_eps;
+    double prune_rel, prune_abs;     // conservative t-pruning margins (DESIGN.md "H3")
+    double background[3], ambient[3];
+    int32_t max_depth;
+    int32_t chunk_first, chunk_step, num_chunks;   // selected 8-row chunks
+    int32_t stack_depth;             // LDS stack entries per lane
+    int32_t pad0;
+    double* out_rgb;                 // packed rows of the selected chunks
+    uint8_t* out_rgba8;
+    unsigned long long* counters;    // [0] shadow rays, [1] secondary rays, [2..6] work counters
+};
+
+constexpr int kMaxDepthGPU = 16;     // mirror/conductor recursion levels kept per lane
+
+}  // namespace myrt

@@ -1,0 +1,994 @@
+// render.hip — MI355X (gfx950) kernels of the renderer core + the rtcore.h C ABI.
+//
+// Hot path (reference: RT/Extensions/Object+Extension.swift:52-379 render loop +
+// trace(); RT/Models/RTContext.swift:476-870 traversal and intersectors):
+//   one lane per pixel, one wave per 8x8 pixel tile (8-row chunks, :75-82),
+//   primary ray with the per-pixel PCG32 jitter -> TLAS/BLAS closest-hit traversal
+//   with FP64 slab tests -> Moeller-Trumbore -> Whitted shading with any-hit shadow
+//   rays -> mirror/conductor bounces, all IEEE binary64 (build with -ffp-contract=off).
+//
+// Traversal visits the surviving nodes in exactly the reference's order (near child
+// first, ties to L; RTContext.swift:600-606).  It additionally prunes nodes whose
+// entry distance exceeds the current closest hit by a conservative margin
+// (tmin > t*(1+prune_rel)+prune_abs), which cannot remove a node holding a hit the
+// reference would accept (DESIGN.md "Pruning").
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/rtcore.h"
+#include "layout.h"
+#include "scene.h"
+
+namespace myrt {
+namespace dev {
+
+#define DINF __builtin_huge_val()
+
+struct V3 { double x, y, z; };
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 ld3(const double* p) { return V3{p[0], p[1], p[2]}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ V3 operator/(V3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ V3 operator+(double s, V3 a) { return {s + a.x, s + a.y, s + a.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, double s) { return {a.x - s, a.y - s, a.z - s}; }
+__device__ __forceinline__ V3 operator+(V3 a, double s) { return {a.x + s, a.y + s, a.z + s}; }
+__device__ __forceinline__ V3 rcp(V3 a) { return {1.0 / a.x, 1.0 / a.y, 1.0 / a.z}; }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ V3 normalize(V3 v) { double r = 1.0 / dsqrt(dot(v, v)); return v * r; }
+__device__ __forceinline__ double length(V3 v) { return dsqrt(dot(v, v)); }
+__device__ __forceinline__ double smax(double x, double y) { return (y >= x) ? y : x; }   // Swift.max
+__device__ __forceinline__ double smin(double x, double y) { return (y < x) ? y : x; }    // Swift.min
+__device__ __forceinline__ bool isfin(V3 v) {
+    return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
+}
+// simd_mul(double4x4, double4) without FMA: ((c0*x + c1*y) + c2*z) + c3*w
+__device__ __forceinline__ V3 m4_point(const double* M, V3 v, double w) {
+    double o[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        double acc = M[0 * 4 + r] * v.x;
+        acc = M[1 * 4 + r] * v.y + acc;
+        acc = M[2 * 4 + r] * v.z + acc;
+        acc = M[3 * 4 + r] * w + acc;
+        o[r] = acc;
+    }
+    return {o[0], o[1], o[2]};
+}
+__device__ __forceinline__ V3 m3_mul(const double* M, V3 v) {
+    double o[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        double acc = M[0 * 3 + r] * v.x;
+        acc = M[1 * 3 + r] * v.y + acc;
+        acc = M[2 * 3 + r] * v.z + acc;
+        o[r] = acc;
+    }
+    return {o[0], o[1], o[2]};
+}
+
+// hitAABB (RTContext.swift:557-565): simd.min/max = fmin/fmax, scalar max/min = Swift's
+__device__ __forceinline__ double slab(double lx, double ly, double lz, double hx, double hy, double hz,
+                                       const V3& o, const V3& inv, double eps) {
+    const double t1x = (lx - o.x) * inv.x, t1y = (ly - o.y) * inv.y, t1z = (lz - o.z) * inv.z;
+    const double t2x = (hx - o.x) * inv.x, t2y = (hy - o.y) * inv.y, t2z = (hz - o.z) * inv.z;
+    const double mnx = fmin(t1x, t2x), mny = fmin(t1y, t2y), mnz = fmin(t1z, t2z);
+    const double mxx = fmax(t1x, t2x), mxy = fmax(t1y, t2y), mxz = fmax(t1z, t2z);
+    const double tmin = smax(smax(mnx, mny), mnz);
+    const double tmax = smin(mxx, smin(mxy, mxz));
+    return (tmax >= smax(tmin, eps)) ? tmin : DINF;
+}
+
+// PCG32 (Object+Extension.swift:556-589)
+struct PCG32 {
+    unsigned long long state, inc;
+    __device__ explicit PCG32(unsigned long long seed) {
+        state = 0ull; inc = (seed << 1) | 1ull;
+        (void)next();
+        state += 0x9E3779B97F4A7C15ull;
+        (void)next();
+    }
+    __device__ __forceinline__ unsigned next() {
+        const unsigned long long old = state;
+        state = old * 6364136223846793005ull + inc;
+        const unsigned xs = (unsigned)(((old >> 18) ^ old) >> 27);
+        const unsigned rot = (unsigned)(old >> 59);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31u));
+    }
+    __device__ __forceinline__ double nextFloat() { return (double)next() * 2.3283064365386963e-10; }
+};
+
+// ----------------------------------------------------------------- traversal stack
+// Per-lane stack: the first kLds entries live in LDS ([slot][lane] so each lane hits
+// its own bank), deeper entries spill to a private array (scratch).  An entry is
+// {ref, entry distance rounded down to float} so far subtrees can be culled at pop.
+constexpr int kLds = 16;
+constexpr int kSpill = 64;
+struct Stack {
+    int2* lds;           // &lds_base[threadIdx.x]; stride blockDim.x
+    int stride;
+    int2 spill[kSpill];
+    int sp;
+    __device__ __forceinline__ void push(int ref, float t) {
+        const int2 e = make_int2(ref, __float_as_int(t));
+        if (sp < kLds) lds[sp * stride] = e; else spill[sp - kLds] = e;
+        ++sp;
+    }
+    __device__ __forceinline__ int2 pop() {
+        --sp;
+        return (sp < kLds) ? lds[sp * stride] : spill[sp - kLds];
+    }
+};
+
+struct Counts { unsigned shadow, secondary; unsigned long long recs, tris, normals, insts; };
+
+struct Hit { double t, u, v; int tri, inst; };
+
+__device__ __forceinline__ float round_down_f(double d) { return __double2float_rd(d); }
+
+// Closest-hit triangle test, intersectTriangle (RTContext.swift:479-510) minus the
+// hit-point/normal writes, which are recomputed once for the final hit (same values).
+__device__ __forceinline__ void tri_closest(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double eps,
+                                           Hit& h, int triIdx, int instIdx) {
+    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+    const V3 pvec = cross(d, e2);
+    const double det = dot(e1, pvec);
+    if (fabs(det) < eps) return;
+    const double invDet = 1.0 / det;
+    const V3 tvec = o_mb - v0;
+    const double u = dot(tvec, pvec) * invDet;
+    if (u < 0.0 || u > 1.0) return;
+    const V3 q = cross(tvec, e1);
+    const double v = dot(d, q) * invDet;
+    if (v < 0.0 || u + v > 1.0) return;
+    const double t = dot(e2, q) * invDet;
+    if (t <= smax(eps, tlo) || t >= h.t) return;
+    h.t = t; h.u = u; h.v = v; h.tri = triIdx; h.inst = instIdx;
+}
+// triShadowHit (RTContext.swift:832-848)
+__device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double thi,
+                                           double eps) {
+    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+    const V3 pvec = cross(d, e2);
+    const double det = dot(e1, pvec);
+    if (fabs(det) < eps) return false;
+    const double invDet = 1.0 / det;
+    const V3 tvec = o_mb - v0;
+    const double u = dot(tvec, pvec) * invDet;
+    if (u < 0.0 || u > 1.0) return false;
+    const V3 q = cross(tvec, e1);
+    const double v = dot(d, q) * invDet;
+    if (v < 0.0 || u + v > 1.0) return false;
+    const double t = dot(e2, q) * invDet;
+    return (t > smax(eps, tlo) && t < thi);
+}
+
+// One ordered BVH walk shared by the closest-hit and any-hit queries.  `ref` is a
+// node the caller has already tested (the root); children are tested at the parent
+// (one 128-B record holds both), near pushed last (RTContext.swift:600-606).
+// LEAF(ref) handles a leaf run and returns true to terminate the walk (any-hit).
+// LIMIT() gives the current pruning distance.
+template <bool COUNT, class Leaf, class Limit>
+__device__ __forceinline__ bool walk(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st, int base,
+                                     Counts& c, Leaf leaf, Limit limit) {
+    const double eps = P.eps;
+    for (;;) {
+        if (ref >= 0) {
+            const WRec& R = P.recs[ref];
+            if (COUNT) c.recs++;
+            double d0 = slab(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv, eps);
+            double d1 = slab(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv, eps);
+            const double lim = limit();
+            if (d0 > lim) d0 = DINF;
+            if (d1 > lim) d1 = DINF;
+            int a = R.ref[0], b = R.ref[1];
+            if (d0 > d1) { const double td = d0; d0 = d1; d1 = td; const int tr = a; a = b; b = tr; }
+            if (d0 != DINF) {
+                if (d1 != DINF) st.push(b, round_down_f(d1));
+                ref = a;
+                continue;
+            }
+        } else {
+            if (leaf(ref)) return true;
+        }
+        // pop, culling entries that start beyond the current limit
+        for (;;) {
+            if (st.sp == base) return false;
+            const int2 e = st.pop();
+            if ((double)__int_as_float(e.y) > limit()) continue;
+            ref = e.x;
+            break;
+        }
+    }
+}
+
+template <bool COUNT>
+__device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
+                                  double time, Hit& h, Stack& st, Counts& c) {
+    const double eps = P.eps;
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    auto limit = [&]() { return h.t * P.prune_rel + P.prune_abs; };   // prune_rel = 1 + delta
+    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
+                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
+    if (d0 == DINF) return;
+    auto tlas_leaf = [&](int ref) -> bool {
+        for (int e = ~ref;; ++e) {
+            const DTlasLeafEntry le = P.tlas_leaf[e];
+            const DInstance& I = P.insts[le.inst];
+            if (COUNT) c.insts++;
+            // world -> local (RTContext.swift:657-673)
+            const V3 instOffset = ld3(I.motion) * time;
+            const V3 ow = o - instOffset;
+            const V3 ol = m4_point(I.w2l, ow, 1.0);
+            const V3 dl = m4_point(I.w2l, d, 0.0);
+            const V3 il = rcp(dl);
+            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                                   I.root_hi[2], ol, il, eps);
+            if (dr != DINF && !(dr > limit())) {
+                const V3 omb = ol - ld3(I.tri_motion) * time;   // Triangle.motionBlur offset (:480-481)
+                const int inst = le.inst;
+                auto blas_leaf = [&](int r) -> bool {
+                    for (int t = ~r;; ++t) {
+                        const TriRec& T = P.tris[t];
+                        if (COUNT) c.tris++;
+                        tri_closest(T, omb, dl, tlo, eps, h, t, inst);
+                        if (T.last) break;
+                    }
+                    return false;
+                };
+                const int sbase = st.sp;
+                if (I.root_ref < 0) blas_leaf(I.root_ref);
+                else walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+            }
+            if (le.last) break;
+        }
+        return false;
+    };
+    const int base = st.sp;
+    if (P.tlas_root_ref < 0) tlas_leaf(P.tlas_root_ref);
+    else walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+}
+
+template <bool COUNT>
+__device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time, Stack& st,
+                         Counts& c) {
+    if (!P.has_tlas) return false;
+    const double eps = P.eps;
+    const V3 inv = rcp(d);
+    const double lim = tmax * P.prune_rel + P.prune_abs;
+    auto limit = [&]() { return lim; };
+    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
+                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
+    if (d0 == DINF || d0 > lim) return false;
+    auto tlas_leaf = [&](int ref) -> bool {
+        for (int e = ~ref;; ++e) {
+            const DTlasLeafEntry le = P.tlas_leaf[e];
+            const DInstance& I = P.insts[le.inst];
+            if (COUNT) c.insts++;
+            const V3 instOffset = ld3(I.motion) * time;
+            const V3 ol = m4_point(I.w2l, o - instOffset, 1.0);
+            const V3 dl = m4_point(I.w2l, d, 0.0);
+            const V3 il = rcp(dl);
+            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                                   I.root_hi[2], ol, il, eps);
+            if (dr != DINF && !(dr > lim)) {
+                const V3 omb = ol - ld3(I.tri_motion) * time;
+                auto blas_leaf = [&](int r) -> bool {
+                    for (int t = ~r;; ++t) {
+                        const TriRec& T = P.tris[t];
+                        if (COUNT) c.tris++;
+                        if (tri_shadow(T, omb, dl, 0.0, tmax, eps)) return true;
+                        if (T.last) break;
+                    }
+                    return false;
+                };
+                const int sbase = st.sp;
+                bool hit;
+                if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
+                else hit = walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+                if (hit) { st.sp = sbase; return true; }
+            }
+            if (le.last) break;
+        }
+        return false;
+    };
+    const int base = st.sp;
+    bool hit;
+    if (P.tlas_root_ref < 0) hit = tlas_leaf(P.tlas_root_ref);
+    else hit = walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+    st.sp = base;
+    return hit;
+}
+
+// orthonormalBasis (Object+Extension.swift:531-552)
+__device__ __forceinline__ void onb(V3 n, V3& tangent, V3& bitangent) {
+    const double sign = n.z >= 0 ? 1.0 : -1.0;
+    const double a = -1.0 / (sign + n.z);
+    const double b = (n.x * n.y) * a;
+    tangent = normalize(v3(1.0 + ((sign * n.x) * n.x) * a, sign * b, (-sign) * n.x));
+    bitangent = normalize(v3(b, sign + (n.y * n.y) * a, -n.y));
+}
+__device__ __forceinline__ V3 reflect(V3 d, V3 n) { return d - (2.0 * dot(d, n)) * n; }
+// fresnelConductorRGB (Object+Extension.swift:493-505)
+__device__ __forceinline__ V3 fresnel_conductor(double eta, double k, double cosI_) {
+    const double cosI = smax(0.0, smin(1.0, fabs(cosI_)));
+    const double cos2 = cosI * cosI;
+    const double eta2k2 = eta * eta + k * k;
+    const double twoEtaCos = (2.0 * eta) * cosI;
+    const V3 cos2v = v3(cos2, cos2, cos2), one = v3(1, 1, 1);
+    const V3 Rs = ((eta2k2 - twoEtaCos) + cos2v) / ((eta2k2 + twoEtaCos) + cos2v);
+    const V3 Rp = (((eta2k2 * cos2v) - twoEtaCos) + one) / (((eta2k2 * cos2v) + twoEtaCos) + one);
+    return 0.5 * (Rs + Rp);
+}
+
+// trace() (Object+Extension.swift:96-283) for diffuse/mirror/conductor materials and
+// point lights.  The recursion Lo + M*trace(depth+1) is run forward and combined
+// backward with the same per-level NaN guard, so the result is the recursive one.
+template <bool COUNT, bool BOUNCE>
+__device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
+                         Counts& c) {
+    V3 Lst[BOUNCE ? kMaxDepthGPU : 1], Mst[BOUNCE ? kMaxDepthGPU : 1];
+    int depth = 0;
+    V3 L;
+    for (;;) {
+        if (!P.has_tlas) { L = v3(0, 0, 0); break; }
+        const V3 inv = rcp(d);
+        Hit h;
+        intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
+        if (h.inst < 0) { L = ld3(P.background); break; }
+        // reconstruct the hit exactly as intersectTriangle + intersectTLAS wrote it
+        const TriRec& T = P.tris[h.tri];
+        const DInstance& I = P.insts[h.inst];
+        const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+        V3 nl;
+        if (I.smooth) {
+            if (COUNT) c.normals++;
+            const double* nn = P.normals + (size_t)h.tri * 9;
+            const double w = 1.0 - h.u - h.v;
+            nl = normalize(((w * ld3(nn)) + (h.u * ld3(nn + 3))) + (h.v * ld3(nn + 6)));
+        } else {
+            nl = normalize(cross(e1, e2));
+        }
+        const V3 pl = (v0 + (h.u * e1)) + (h.v * e2);
+        const V3 p = m4_point(I.l2w, pl, 1.0) + ld3(I.motion) * time;
+        V3 Ngeo = normalize(m3_mul(I.nmat, nl));
+        if (I.det_neg) Ngeo = -Ngeo;
+        const int matIndex = max(0, min(P.num_mats - 1, I.material - 1));
+        const DMaterial& M = P.mats[matIndex];
+        const bool frontFacing = dot(d, Ngeo) < 0;
+        const V3 N = frontFacing ? Ngeo : -Ngeo;
+        const bool computeDirect = !(M.ior > 0) || frontFacing;
+        V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+        if (computeDirect) {
+            for (int li = 0; li < P.num_plights; ++li) {
+                const DPointLight& PL = P.plights[li];
+                V3 wi = ld3(PL.position) - p;
+                const double dist = length(wi);
+                wi = normalize(wi);
+                const V3 so = p + wi * P.shadow_eps;
+                c.shadow++;
+                const bool blocked = occluded<COUNT>(P, so, wi, dist, time, st, c);
+                if (!blocked) {
+                    const double NdotL = smax(0.0, dot(N, wi));
+                    if (NdotL > 0) {
+                        const double shininess = smax(1.0, M.phong);
+                        const V3 Ld = ld3(M.diffuse) * NdotL;
+                        const V3 view = normalize(-d);
+                        const V3 hv = normalize(wi + view);
+                        const double NdotH = smax(0.0, dot(N, hv));
+                        const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
+                        const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
+                        Lo = Lo + (Ld + Ls) * atten;
+                    }
+                }
+            }
+        }
+        if (BOUNCE && (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && depth < P.max_depth &&
+            depth < kMaxDepthGPU) {
+            V3 mult;
+            if (M.type == RT_MAT_MIRROR) {
+                mult = ld3(M.mirror);
+            } else {
+                const double cosI = smax(0.0, -dot(d, N));
+                mult = fresnel_conductor(M.ior, M.absorption_index, cosI) * ld3(M.mirror);
+            }
+            V3 rd = normalize(reflect(d, N));
+            if (M.roughness != 0.0) {
+                V3 t, b;
+                onb(rd, t, b);
+                const double r1 = rng.nextFloat() - 0.5;
+                const double r2 = rng.nextFloat() - 0.5;
+                rd = (rd + (M.roughness * r1) * b) + (M.roughness * r2) * t;
+                rd = normalize(rd);
+            }
+            Lst[depth] = Lo; Mst[depth] = mult;
+            depth++;
+            c.secondary++;
+            o = p + N * P.shadow_eps;
+            d = rd;
+            tlo = 0.0;
+            continue;
+        }
+        L = isfin(Lo) ? Lo : v3(0, 0, 0);
+        break;
+    }
+    if (BOUNCE) {
+        for (int q = depth - 1; q >= 0; --q) {
+            const V3 Lo = Lst[q] + Mst[q] * L;
+            L = isfin(Lo) ? Lo : v3(0, 0, 0);
+        }
+    }
+    return L;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+// One block = 256 lanes = 4 waves; each wave renders an 8x8 tile of one 8-row chunk.
+template <bool COUNT, bool BOUNCE>
+__global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
+    extern __shared__ int2 lds_stack[];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int i = blockIdx.x * 32 + wave * 8 + (lane & 7);
+    const int slot = blockIdx.y;                       // position in the selected chunk list
+    const int chunk = P.chunk_first + slot * P.chunk_step;
+    const int rowInChunk = lane >> 3;
+    const int j = chunk * 8 + rowInChunk;
+    const DCamera& C = P.cam;
+    const bool valid = (i < C.width) && (j < C.height);
+    Counts cnt{0, 0, 0, 0, 0, 0};
+    if (valid) {
+        Stack st;
+        st.lds = lds_stack + tid;
+        st.stride = blockDim.x;
+        st.sp = 0;
+        PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
+        V3 pixel = v3(0, 0, 0);
+        const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
+        const int n = C.n;
+        int sampleIndex = 0;
+        for (int sy = 0; sy < n && sampleIndex < C.samples; ++sy) {
+            for (int sx = 0; sx < n; ++sx) {
+                const double xi1 = rng.nextFloat();
+                const double xi2 = rng.nextFloat();
+                const double iOffset = ((double)sx + xi1) / (double)n;
+                const double jOffset = ((double)sy + xi2) / (double)n;
+                const double currentI = (double)i + iOffset;
+                const double currentJ = (double)j + jOffset;
+                const V3 vOff = v * (currentJ * C.dv);
+                const V3 rowTopLeft = q00 - vOff;
+                const V3 uOff = u * (currentI * C.du);
+                const V3 s = rowTopLeft + uOff;
+                const V3 dir0 = normalize(s - eye);
+                V3 dir = dir0, camEye = eye;
+                if (C.aperture > 0 && C.focus > 0) {                  // DOF (:325-338)
+                    const V3 forward = -w;
+                    const double denom = dot(dir0, forward);
+                    const double tFocus = fabs(denom) < 1e-6 ? C.focus : (C.focus / denom);
+                    const V3 pFocus = eye + dir0 * tFocus;
+                    const double uRand = rng.nextFloat() - 0.5;
+                    const double vRand = rng.nextFloat() - 0.5;
+                    const V3 lensOffset = ((uRand * u) + (vRand * v)) * C.aperture;
+                    const V3 a = eye + lensOffset;
+                    dir = normalize(pFocus - a);
+                    camEye = a;
+                }
+                const double time = rng.nextFloat();
+                const double denom = dot(dir, w);
+                const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
+                const double tlo = smax(tImg, 0.0);
+                const V3 col = trace_path<COUNT, BOUNCE>(P, camEye, dir, tlo, time, rng, st, cnt);
+                pixel = pixel + col;
+                sampleIndex += 1;
+                if (sampleIndex >= C.samples) break;
+            }
+        }
+        const V3 px = pixel / (double)C.samples;
+        const size_t row = (size_t)slot * 8 + rowInChunk;
+        const size_t o = row * (size_t)C.width + i;
+        if (P.out_rgb) {
+            P.out_rgb[o * 3 + 0] = px.x;
+            P.out_rgb[o * 3 + 1] = px.y;
+            P.out_rgb[o * 3 + 2] = px.z;
+        }
+        if (P.out_rgba8) {                                           // RayTracer.swift:186-195
+            const double cx = fmin(fmax(px.x, 0.0), 255.0), cy = fmin(fmax(px.y, 0.0), 255.0),
+                         cz = fmin(fmax(px.z, 0.0), 255.0);
+            const unsigned packed = (unsigned)(unsigned char)cx | ((unsigned)(unsigned char)cy << 8) |
+                                    ((unsigned)(unsigned char)cz << 16) | (255u << 24);
+            reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
+        }
+    }
+    // ray / work counters: one atomic per wave
+    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary);
+    if (lane == 0) {
+        if (s0) atomicAdd(&P.counters[0], s0);
+        if (s1) atomicAdd(&P.counters[1], s1);
+    }
+    if (COUNT) {
+        const unsigned long long a = wave_sum(cnt.recs), b = wave_sum(cnt.tris), cc = wave_sum(cnt.normals),
+                                 dd = wave_sum(cnt.insts), ee = wave_sum(valid ? 1ull : 0ull);
+        if (lane == 0) {
+            atomicAdd(&P.counters[2], a); atomicAdd(&P.counters[3], b); atomicAdd(&P.counters[4], cc);
+            atomicAdd(&P.counters[5], dd); atomicAdd(&P.counters[6], ee);
+        }
+    }
+}
+
+}  // namespace dev
+}  // namespace myrt
+
+// ================================================================== host side / C ABI
+using namespace myrt;
+
+namespace {
+
+thread_local std::string g_err;
+static int32_t fail(int32_t code, const std::string& msg) { g_err = msg; return code; }
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess) return fail(RT_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+struct DeviceReplica {
+    int device = 0;
+    WRec* recs = nullptr;
+    TriRec* tris = nullptr;
+    double* normals = nullptr;
+    DInstance* insts = nullptr;
+    DTlasLeafEntry* tlas_leaf = nullptr;
+    DMaterial* mats = nullptr;
+    DPointLight* plights = nullptr;
+    unsigned long long* counters = nullptr;   // 8 x u64
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int64_t bytes = 0;
+};
+
+}  // namespace
+
+struct rt_scene {
+    HostScene host;
+    std::vector<DeviceReplica> devs;
+    std::mutex mu;
+    double upload_ms = 0;
+};
+
+template <class T>
+static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
+    const size_t n = std::max<size_t>(1, v.size());
+    HIP_TRY(hipMalloc((void**)dst, n * sizeof(T)));
+    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    bytes += (int64_t)(n * sizeof(T));
+    return RT_OK;
+}
+
+static void free_replica(DeviceReplica& r) {
+    (void)hipSetDevice(r.device);
+    (void)hipFree(r.recs); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
+    (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
+    if (r.ev0) (void)hipEventDestroy(r.ev0);
+    if (r.ev1) (void)hipEventDestroy(r.ev1);
+    if (r.stream) (void)hipStreamDestroy(r.stream);
+    r = DeviceReplica();
+}
+
+static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r) {
+    r.device = device;
+    HIP_TRY(hipSetDevice(device));
+    int32_t rc;
+    if ((rc = upload(S.recs, &r.recs, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.normals, &r.normals, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.tlas_leaf, &r.tlas_leaf, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.mats, &r.mats, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.plights, &r.plights, r.bytes)) != RT_OK) return rc;
+    HIP_TRY(hipMalloc((void**)&r.counters, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&r.ev0));
+    HIP_TRY(hipEventCreate(&r.ev1));
+    return RT_OK;
+}
+
+// makeCameraBasis + frame constants (Object+Extension.swift:58-93, 382-427), on the host
+static DCamera camera_constants(const rt_camera& cam) {
+    auto nrm = [](const double a[3], double o[3]) {
+        const double r = 1.0 / std::sqrt((a[0] * a[0] + a[1] * a[1]) + a[2] * a[2]);
+        o[0] = a[0] * r; o[1] = a[1] * r; o[2] = a[2] * r;
+    };
+    auto crs = [](const double a[3], const double b[3], double o[3]) {
+        o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    DCamera C{};
+    const int width = std::max(1, cam.width), height = std::max(1, cam.height);
+    const double aspect = double(width) / double(height);
+    const double e[3] = {cam.position.x, cam.position.y, cam.position.z};
+    const double nd = cam.near_distance;
+    double l, r, b, t, w[3], u[3], v[3], gn[3], un[3], tmp[3];
+    const double up[3] = {cam.up.x, cam.up.y, cam.up.z};
+    if (cam.type == RT_CAM_LOOKAT) {
+        const double gaze[3] = {cam.gaze_point.x - cam.position.x, cam.gaze_point.y - cam.position.y,
+                                cam.gaze_point.z - cam.position.z};
+        nrm(gaze, gn);
+        if (!std::isnan(cam.fovy)) {
+            const double fovYRad = (cam.fovy * M_PI) / (2.0 * 180.0);
+            t = nd * std::tan(fovYRad);
+        } else {
+            t = nd * 0.5;
+        }
+        b = -t; r = t * aspect; l = -r;
+    } else {
+        const double gaze[3] = {cam.gaze.x, cam.gaze.y, cam.gaze.z};
+        nrm(gaze, gn);
+        l = cam.near_plane[0]; r = cam.near_plane[1]; b = cam.near_plane[2]; t = cam.near_plane[3];
+    }
+    w[0] = -gn[0]; w[1] = -gn[1]; w[2] = -gn[2];
+    nrm(up, un);
+    crs(un, w, tmp); nrm(tmp, u);
+    crs(w, u, tmp); nrm(tmp, v);
+    const double du = (r - l) / double(width), dv = (t - b) / double(height);
+    double m[3], q00[3];
+    for (int k = 0; k < 3; ++k) m[k] = e[k] - w[k] * nd;
+    for (int k = 0; k < 3; ++k) q00[k] = (m[k] + u[k] * l) + v[k] * t;
+    for (int k = 0; k < 3; ++k) { C.eye[k] = e[k]; C.u[k] = u[k]; C.v[k] = v[k]; C.w[k] = w[k]; C.q00[k] = q00[k]; }
+    C.du = du; C.dv = dv; C.nd = nd;
+    C.aperture = cam.aperture_size; C.focus = cam.focus_distance;
+    C.width = width; C.height = height;
+    C.samples = std::max(1, cam.num_samples);
+    C.n = (int)std::sqrt((double)C.samples);
+    return C;
+}
+
+static int32_t check_renderable(const HostScene& S, int32_t cam) {
+    if (cam < 0 || cam >= (int32_t)S.cams.size()) return fail(RT_ERR_INVALID_CAMERA, "Invalid camera index");
+    if (S.has_dielectric) return fail(RT_ERR_UNSUPPORTED, "dielectric materials are not implemented on the GPU path yet");
+    if (S.num_area_lights > 0) return fail(RT_ERR_UNSUPPORTED, "area lights are not implemented on the GPU path yet");
+    if (S.max_depth > kMaxDepthGPU) return fail(RT_ERR_UNSUPPORTED, "maxRecursionDepth above the GPU limit");
+    return RT_OK;
+}
+
+static int32_t num_chunks_total(int32_t height) { return (std::max(1, height) + 7) / 8; }
+
+extern "C" int32_t rt_rows_for_chunks(int32_t height, int32_t chunk_first, int32_t chunk_step) {
+    if (chunk_step < 1 || chunk_first < 0) return 0;
+    height = std::max(1, height);
+    int32_t rows = 0;
+    for (int32_t c = chunk_first; c < num_chunks_total(height); c += chunk_step) rows += std::min(8, height - 8 * c);
+    return rows;
+}
+
+static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32_t cam, int32_t first, int32_t step,
+                                double* out_rgb, uint8_t* out_rgba8) {
+    const HostScene& S = s->host;
+    RenderParams P{};
+    P.recs = r.recs; P.tris = r.tris; P.normals = r.normals; P.insts = r.insts; P.tlas_leaf = r.tlas_leaf;
+    P.mats = r.mats; P.plights = r.plights;
+    for (int k = 0; k < 3; ++k) { P.tlas_root_lo[k] = S.tlas_root_lo[k]; P.tlas_root_hi[k] = S.tlas_root_hi[k]; }
+    P.tlas_root_ref = S.tlas_root_ref;
+    P.has_tlas = S.has_tlas ? 1 : 0;
+    P.num_mats = (int32_t)S.mats.size();
+    P.num_plights = (int32_t)S.plights.size();
+    P.cam = camera_constants(S.cams[cam]);
+    P.eps = S.eps; P.shadow_eps = S.shadow_eps;
+    P.prune_rel = 1.0 + 1e-7;
+    P.prune_abs = 1e-9 * S.scene_extent;
+    for (int k = 0; k < 3; ++k) { P.background[k] = S.background[k]; P.ambient[k] = S.ambient[k]; }
+    P.max_depth = S.max_depth;
+    P.chunk_first = first; P.chunk_step = step;
+    int32_t nsel = 0;
+    for (int32_t c = first; c < num_chunks_total(P.cam.height); c += step) nsel++;
+    P.num_chunks = nsel;
+    P.stack_depth = dev::kLds;
+    P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
+    P.counters = r.counters;
+    return P;
+}
+
+static bool scene_has_bounce(const HostScene& S) {
+    for (const auto& m : S.mats) if (m.type == RT_MAT_MIRROR || m.type == RT_MAT_CONDUCTOR) return true;
+    return false;
+}
+
+static int32_t launch(const rt_scene* s, const DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {
+    if (P.num_chunks == 0) return RT_OK;
+    dim3 grid((unsigned)((P.cam.width + 31) / 32), (unsigned)P.num_chunks, 1);
+    dim3 block(256, 1, 1);
+    const size_t lds = (size_t)dev::kLds * 256 * sizeof(int2);
+    const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
+    if (count) {
+        if (bounce) hipLaunchKernelGGL((dev::render_kernel<true, true>), grid, block, lds, stream, P);
+        else hipLaunchKernelGGL((dev::render_kernel<true, false>), grid, block, lds, stream, P);
+    } else {
+        if (bounce) hipLaunchKernelGGL((dev::render_kernel<false, true>), grid, block, lds, stream, P);
+        else hipLaunchKernelGGL((dev::render_kernel<false, false>), grid, block, lds, stream, P);
+    }
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+const char* rt_version(void) { return "myraytracer_amd 0.1 (gfx950, fp64)"; }
+
+int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32_t n_devices, rt_scene** out) {
+    if (!out) return fail(RT_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    if (!desc) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+    try {
+        auto* s = new rt_scene();
+        std::string err;
+        int32_t rc = build_host_scene(desc, s->host, err);
+        if (rc != RT_OK) { delete s; return fail(rc, err); }
+        std::vector<int> devs;
+        if (n_devices <= 0 || !devices) devs.push_back(0);
+        else for (int k = 0; k < n_devices; ++k) devs.push_back(devices[k]);
+        auto t0 = std::chrono::steady_clock::now();
+        s->devs.resize(devs.size());
+        for (size_t k = 0; k < devs.size(); ++k) {
+            rc = make_replica(s->host, devs[k], s->devs[k]);
+            if (rc != RT_OK) {
+                std::string e = g_err;
+                for (auto& r : s->devs) free_replica(r);
+                delete s;
+                return fail(rc, e);
+            }
+        }
+        s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        // device copies are authoritative; drop the large host arrays
+        s->host.recs.clear(); s->host.recs.shrink_to_fit();
+        s->host.tris.clear(); s->host.tris.shrink_to_fit();
+        s->host.normals.clear(); s->host.normals.shrink_to_fit();
+        *out = s;
+        return RT_OK;
+    } catch (const std::bad_alloc&) {
+        return fail(RT_ERR_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_INVALID_ARG, e.what());
+    }
+}
+
+void rt_scene_destroy(rt_scene* s) {
+    if (!s) return;
+    for (auto& r : s->devs) free_replica(r);
+    delete s;
+}
+
+int32_t rt_scene_info_get(const rt_scene* s, rt_scene_info* out) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
+    if (!out) return fail(RT_ERR_INVALID_ARG, "out is NULL");
+    const HostScene& S = s->host;
+    out->meshes = S.n_meshes; out->triangles = S.n_tris; out->spheres = S.n_spheres; out->planes = S.n_planes;
+    out->instances = (int64_t)S.insts.size();
+    out->blas_nodes = S.blas_records; out->tlas_nodes = S.tlas_records; out->max_depth = S.max_stack;
+    out->build_ms = S.build_ms; out->upload_ms = s->upload_ms;
+    out->device_bytes = s->devs.empty() ? 0 : s->devs[0].bytes;
+    return RT_OK;
+}
+
+int32_t rt_render_device(rt_scene* s, int32_t slot, int32_t cam, int32_t first, int32_t step, double* d_rgb,
+                         uint8_t* d_rgba8, void* stream) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+    if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
+    if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
+    int32_t rc = check_renderable(s->host, cam);
+    if (rc != RT_OK) return rc;
+    DeviceReplica& r = s->devs[slot];
+    HIP_TRY(hipSetDevice(r.device));
+    hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
+    HIP_TRY(hipMemsetAsync(r.counters, 0, 8 * sizeof(unsigned long long), st));
+    RenderParams P = make_params(s, r, cam, first, step, d_rgb, d_rgba8);
+    return launch(s, r, P, st, false);
+}
+
+int32_t rt_stats_collect(rt_scene* s, int32_t slot, rt_stats* stats) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
+    if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
+    DeviceReplica& r = s->devs[slot];
+    HIP_TRY(hipSetDevice(r.device));
+    unsigned long long c[8];
+    HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
+    if (stats) { stats->shadow_rays = (int64_t)c[0]; stats->secondary_rays = (int64_t)c[1]; }
+    return RT_OK;
+}
+
+int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t first, int32_t step, double* d_rgb,
+                                 void* stream, rt_work_counters* out) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+    if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
+    int32_t rc = check_renderable(s->host, cam);
+    if (rc != RT_OK) return rc;
+    DeviceReplica& r = s->devs[slot];
+    HIP_TRY(hipSetDevice(r.device));
+    hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
+    HIP_TRY(hipMemsetAsync(r.counters, 0, 8 * sizeof(unsigned long long), st));
+    RenderParams P = make_params(s, r, cam, first, step, d_rgb, nullptr);
+    rc = launch(s, r, P, st, true);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    unsigned long long c[8];
+    HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
+    if (out) {
+        out->records_fetched = (int64_t)c[2]; out->tri_tests = (int64_t)c[3]; out->normal_fetches = (int64_t)c[4];
+        out->instance_entries = (int64_t)c[5]; out->pixels = (int64_t)c[6];
+    }
+    return RT_OK;
+}
+
+// Host-buffer render across all device replicas: chunk k of the selection goes to
+// replica (k mod D); each replica renders its share into device memory, copies it back
+// and the host scatters its rows into the packed output (no collective involved).
+int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb, uint8_t* out_rgba8,
+                  rt_stats* stats, rt_progress_fn progress, void* user) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+    if (s->devs.empty()) return fail(RT_ERR_NO_RENDERER, "Renderer not initialized.");
+    if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
+    int32_t rc = check_renderable(s->host, cam);
+    if (rc != RT_OK) return rc;
+    std::lock_guard<std::mutex> lock(s->mu);
+    auto t0 = std::chrono::steady_clock::now();
+    const rt_camera& C = s->host.cams[cam];
+    const int32_t W = std::max(1, C.width), H = std::max(1, C.height);
+    std::vector<int32_t> sel;
+    for (int32_t c = first; c < num_chunks_total(H); c += step) sel.push_back(c);
+    const int32_t D = (int32_t)s->devs.size();
+    std::vector<int32_t> rowOff(sel.size() + 1, 0);
+    for (size_t q = 0; q < sel.size(); ++q) rowOff[q + 1] = rowOff[q] + std::min(8, H - 8 * sel[q]);
+    std::vector<int32_t> codes(D, RT_OK);
+    std::vector<std::string> errs(D);
+    std::vector<double> kms(D, 0.0);
+    std::vector<unsigned long long> shadow(D, 0), secondary(D, 0);
+    auto work = [&](int32_t k) {
+        DeviceReplica& r = s->devs[k];
+        auto body = [&]() -> int32_t {
+            HIP_TRY(hipSetDevice(r.device));
+            const int32_t myFirst = first + k * step, myStep = step * D;
+            const int32_t rows = rt_rows_for_chunks(H, myFirst, myStep);
+            if (rows == 0) return RT_OK;
+            double* d_rgb = nullptr; uint8_t* d_rgba = nullptr;
+            HIP_TRY(hipMalloc((void**)&d_rgb, (size_t)rows * W * 3 * sizeof(double)));
+            if (out_rgba8) HIP_TRY(hipMalloc((void**)&d_rgba, (size_t)rows * W * 4));
+            HIP_TRY(hipMemsetAsync(r.counters, 0, 8 * sizeof(unsigned long long), r.stream));
+            RenderParams P = make_params(s, r, cam, myFirst, myStep, d_rgb, d_rgba);
+            HIP_TRY(hipEventRecord(r.ev0, r.stream));
+            int32_t lrc = launch(s, r, P, r.stream, false);
+            if (lrc != RT_OK) { (void)hipFree(d_rgb); (void)hipFree(d_rgba); return lrc; }
+            HIP_TRY(hipEventRecord(r.ev1, r.stream));
+            std::vector<double> h_rgb((size_t)rows * W * 3);
+            std::vector<uint8_t> h_rgba(out_rgba8 ? (size_t)rows * W * 4 : 0);
+            HIP_TRY(hipMemcpyAsync(h_rgb.data(), d_rgb, h_rgb.size() * sizeof(double), hipMemcpyDeviceToHost, r.stream));
+            if (out_rgba8) HIP_TRY(hipMemcpyAsync(h_rgba.data(), d_rgba, h_rgba.size(), hipMemcpyDeviceToHost, r.stream));
+            unsigned long long c[8];
+            HIP_TRY(hipMemcpyAsync(c, r.counters, sizeof(c), hipMemcpyDeviceToHost, r.stream));
+            HIP_TRY(hipStreamSynchronize(r.stream));
+            float ms = 0; (void)hipEventElapsedTime(&ms, r.ev0, r.ev1);
+            kms[k] = ms; shadow[k] = c[0]; secondary[k] = c[1];
+            (void)hipFree(d_rgb); (void)hipFree(d_rgba);
+            // scatter: my q-th chunk is selection entry k + q*D
+            int32_t srcRow = 0;
+            for (size_t q = k; q < sel.size(); q += D) {
+                const int32_t nr = rowOff[q + 1] - rowOff[q];
+                if (out_rgb) std::memcpy(out_rgb + (size_t)rowOff[q] * W * 3, h_rgb.data() + (size_t)srcRow * W * 3, (size_t)nr * W * 3 * sizeof(double));
+                if (out_rgba8) std::memcpy(out_rgba8 + (size_t)rowOff[q] * W * 4, h_rgba.data() + (size_t)srcRow * W * 4, (size_t)nr * W * 4);
+                srcRow += nr;
+            }
+            return RT_OK;
+        };
+        codes[k] = body();
+        errs[k] = g_err;
+    };
+    if (D == 1) work(0);
+    else {
+        std::vector<std::thread> th;
+        for (int32_t k = 0; k < D; ++k) th.emplace_back(work, k);
+        for (auto& t : th) t.join();
+    }
+    for (int32_t k = 0; k < D; ++k) if (codes[k] != RT_OK) return fail(codes[k], errs[k]);
+    if (progress && !progress(user, rowOff.back(), rowOff.back())) return fail(RT_ERR_CANCELLED, "cancelled");
+    if (stats) {
+        stats->meshes = s->host.n_meshes; stats->triangles = s->host.n_tris;
+        stats->spheres = s->host.n_spheres; stats->planes = s->host.n_planes;
+        const int64_t n = (int64_t)std::sqrt((double)std::max(1, C.num_samples));
+        stats->primary_rays = (int64_t)rowOff.back() * W * n * n;
+        int64_t sh = 0, se = 0; double km = 0;
+        for (int32_t k = 0; k < D; ++k) { sh += (int64_t)shadow[k]; se += (int64_t)secondary[k]; km = std::max(km, kms[k]); }
+        stats->shadow_rays = sh; stats->secondary_rays = se; stats->kernel_ms = km;
+        stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return RT_OK;
+}
+
+// ---- PLY
+int32_t rt_ply_load(const char* path, rt_ply_mesh* out) {
+    if (!out) return fail(RT_ERR_INVALID_ARG, "out is NULL");
+    std::memset(out, 0, sizeof(*out));
+    std::vector<double> pos, nrm; std::vector<float> uv; std::vector<int32_t> idx;
+    std::string err;
+    try {
+        int32_t rc = ply_load(path, pos, nrm, uv, idx, err);
+        if (rc != RT_OK) return fail(rc, err);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_PLY, e.what());
+    }
+    auto dup = [](const auto& v, auto** dst) {
+        using T = typename std::decay_t<decltype(v)>::value_type;
+        *dst = v.empty() ? nullptr : static_cast<T*>(std::malloc(v.size() * sizeof(T)));
+        if (*dst) std::memcpy(*dst, v.data(), v.size() * sizeof(T));
+    };
+    dup(pos, &out->positions); out->num_positions = (int64_t)pos.size() / 3;
+    dup(nrm, &out->normals); out->num_normals = (int64_t)nrm.size() / 3;
+    dup(uv, &out->texcoords); out->num_texcoords = (int64_t)uv.size() / 2;
+    dup(idx, &out->indices); out->num_indices = (int64_t)idx.size();
+    return RT_OK;
+}
+
+void rt_ply_free(rt_ply_mesh* m) {
+    if (!m) return;
+    std::free(m->positions); std::free(m->normals); std::free(m->texcoords); std::free(m->indices);
+    std::memset(m, 0, sizeof(*m));
+}
+
+// ---- debug / test hooks ---------------------------------------------------------------
+// Host-only scene build (no device): BVH hashes per instance (+ TLAS at [n]) and info.
+int32_t rt_debug_host_build(const rt_scene_desc* desc, uint64_t* hashes, int32_t max_hashes, int32_t* n_instances,
+                            rt_scene_info* info) {
+    if (!desc) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
+    try {
+        HostScene S;
+        std::string err;
+        int32_t rc = build_host_scene(desc, S, err);
+        if (rc != RT_OK) return fail(rc, err);
+        const int32_t n = (int32_t)S.inst_bvh_hash.size();
+        if (n_instances) *n_instances = n;
+        if (hashes) {
+            for (int32_t k = 0; k < n && k < max_hashes; ++k) hashes[k] = S.inst_bvh_hash[k];
+            if (n < max_hashes) hashes[n] = S.tlas_hash;
+        }
+        if (info) {
+            std::memset(info, 0, sizeof(*info));
+            info->meshes = S.n_meshes; info->triangles = S.n_tris; info->instances = n;
+            info->blas_nodes = S.blas_records; info->tlas_nodes = S.tlas_records; info->max_depth = S.max_stack;
+            info->build_ms = S.build_ms;
+            info->device_bytes = (int64_t)(S.recs.size() * sizeof(WRec) + S.tris.size() * sizeof(TriRec) +
+                                           S.normals.size() * sizeof(double));
+        }
+        return RT_OK;
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_INVALID_ARG, e.what());
+    }
+}
+
+// ---- debug: canonical BVH hashes (tests compare them with the oracle's)
+uint64_t rt_debug_bvh_hash(const rt_scene* s, int32_t instance) {
+    if (!s) return 0;
+    if (instance < 0) return s->host.tlas_hash;
+    if (instance >= (int32_t)s->host.inst_bvh_hash.size()) return 0;
+    return s->host.inst_bvh_hash[instance];
+}
+
+}  // extern "C"

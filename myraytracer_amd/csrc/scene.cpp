@@ -1,0 +1,632 @@
+// scene.cpp — host scene construction (product code; see scene.h).
+//
+// Arithmetic that feeds the kernels (edges, centroids, SAH costs, transformed
+// bounds) follows the Swift expression order literally so the BVH is the
+// reference's BVH bit for bit; compile with -ffp-contract=off.
+#include "scene.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+
+namespace myrt {
+
+static const double kInf = std::numeric_limits<double>::infinity();
+
+// ------------------------------------------------------------------ small math
+struct D3 { double x, y, z; };
+static inline D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+static inline D3 operator+(D3 a, D3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static inline D3 operator-(D3 a, D3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline D3 operator*(D3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+static inline D3 operator*(double s, D3 a) { return {s * a.x, s * a.y, s * a.z}; }
+static inline D3 operator/(D3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
+static inline double dot(D3 a, D3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static inline D3 cross(D3 a, D3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+static inline D3 normalize(D3 v) { double r = 1.0 / std::sqrt(dot(v, v)); return v * r; }
+static inline D3 vmin(D3 a, D3 b) { return {std::fmin(a.x, b.x), std::fmin(a.y, b.y), std::fmin(a.z, b.z)}; }
+static inline D3 vmax(D3 a, D3 b) { return {std::fmax(a.x, b.x), std::fmax(a.y, b.y), std::fmax(a.z, b.z)}; }
+static inline D3 of(rt_vec3 v) { return {v.x, v.y, v.z}; }
+static inline double smin(double x, double y) { return (y < x) ? y : x; }   // Swift.min
+static inline double smax(double x, double y) { return (y >= x) ? y : x; }  // Swift.max
+
+// ------------------------------------------------------- reference-exact BVH build
+// BVHBuilder.init/subdivide/findBestSplitPlane (BVH.swift:78-250).
+namespace {
+struct Builder {
+    const PrimSet& P;
+    RefBVH& B;
+    int maxLeaf, N;
+    // scratch reused across nodes
+    std::vector<double> binLo, binHi;   // [axis][bin][3]
+    std::vector<int64_t> binCnt;        // [axis][bin]
+
+    Builder(const PrimSet& p, RefBVH& b, int ml, int bins) : P(p), B(b), maxLeaf(ml), N(std::max(2, bins)) {
+        binLo.resize(3 * N * 3); binHi.resize(3 * N * 3); binCnt.resize(3 * N);
+    }
+    void updateNodeBounds(int64_t idx) {                                  // :108-124
+        D3 mn = d3(kInf, kInf, kInf), mx = d3(-kInf, -kInf, -kInf);
+        const int64_t first = B.leftFirst[idx], cnt = B.count[idx];
+        for (int64_t i = 0; i < cnt; ++i) {
+            const int64_t p = B.primIdx[first + i];
+            mn = vmin(mn, d3(P.bmin[3 * p], P.bmin[3 * p + 1], P.bmin[3 * p + 2]));
+            mx = vmax(mx, d3(P.bmax[3 * p], P.bmax[3 * p + 1], P.bmax[3 * p + 2]));
+        }
+        B.lo[3 * idx] = mn.x; B.lo[3 * idx + 1] = mn.y; B.lo[3 * idx + 2] = mn.z;
+        B.hi[3 * idx] = mx.x; B.hi[3 * idx + 1] = mx.y; B.hi[3 * idx + 2] = mx.z;
+    }
+    static inline double area(const double* lo, const double* hi) {      // AABB.swift:29-33
+        const double ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+        return 2.0 * ((ex * ey + ey * ez) + ez * ex);
+    }
+    // returns bestAxis/bestPos exactly as findBestSplitPlane (BVH.swift:192-250)
+    void findBestSplitPlane(int64_t first, int64_t count, int& axis, double& splitPos) {
+        double bestCost = kInf;
+        double cmin[3] = {kInf, kInf, kInf}, cmax[3] = {-kInf, -kInf, -kInf};
+        for (int64_t i = 0; i < count; ++i) {
+            const double* c = &P.cen[3 * B.primIdx[first + i]];
+            for (int a = 0; a < 3; ++a) { cmin[a] = smin(cmin[a], c[a]); cmax[a] = smax(cmax[a], c[a]); }
+        }
+        bool valid[3];
+        double scale[3];
+        for (int a = 0; a < 3; ++a) {
+            valid[a] = !(cmax[a] <= cmin[a]);
+            scale[a] = valid[a] ? double(N) / (cmax[a] - cmin[a]) : 0.0;
+            for (int b = 0; b < N; ++b) {
+                binCnt[a * N + b] = 0;
+                for (int k = 0; k < 3; ++k) { binLo[(a * N + b) * 3 + k] = kInf; binHi[(a * N + b) * 3 + k] = -kInf; }
+            }
+        }
+        for (int64_t i = 0; i < count; ++i) {
+            const int64_t p = B.primIdx[first + i];
+            const double* c = &P.cen[3 * p];
+            const double* pl = &P.bmin[3 * p];
+            const double* ph = &P.bmax[3 * p];
+            for (int a = 0; a < 3; ++a) {
+                if (!valid[a]) continue;
+                int64_t q = (int64_t)((c[a] - cmin[a]) * scale[a]);
+                int64_t idx = (q < (int64_t)(N - 1)) ? q : (int64_t)(N - 1);
+                binCnt[a * N + idx] += 1;
+                double* bl = &binLo[(a * N + idx) * 3];
+                double* bh = &binHi[(a * N + idx) * 3];
+                for (int k = 0; k < 3; ++k) { bl[k] = std::fmin(bl[k], pl[k]); bh[k] = std::fmax(bh[k], ph[k]); }
+            }
+        }
+        double leftArea[64], rightArea[64];
+        int64_t leftCnt[64], rightCnt[64];
+        for (int a = 0; a < 3; ++a) {
+            if (!valid[a]) continue;
+            double Llo[3] = {kInf, kInf, kInf}, Lhi[3] = {-kInf, -kInf, -kInf};
+            double Rlo[3] = {kInf, kInf, kInf}, Rhi[3] = {-kInf, -kInf, -kInf};
+            int64_t sL = 0, sR = 0;
+            for (int i = 0; i < N - 1; ++i) {
+                sL += binCnt[a * N + i]; leftCnt[i] = sL;
+                for (int k = 0; k < 3; ++k) {
+                    Llo[k] = std::fmin(Llo[k], binLo[(a * N + i) * 3 + k]);
+                    Lhi[k] = std::fmax(Lhi[k], binHi[(a * N + i) * 3 + k]);
+                }
+                leftArea[i] = area(Llo, Lhi);
+                const int rb = N - 1 - i;
+                sR += binCnt[a * N + rb]; rightCnt[N - 2 - i] = sR;
+                for (int k = 0; k < 3; ++k) {
+                    Rlo[k] = std::fmin(Rlo[k], binLo[(a * N + rb) * 3 + k]);
+                    Rhi[k] = std::fmax(Rhi[k], binHi[(a * N + rb) * 3 + k]);
+                }
+                rightArea[N - 2 - i] = area(Rlo, Rhi);
+            }
+            const double step = (cmax[a] - cmin[a]) / double(N);
+            for (int i = 0; i < N - 1; ++i) {
+                if (leftCnt[i] == 0 || rightCnt[i] == 0) continue;
+                const double cost = double(leftCnt[i]) * leftArea[i] + double(rightCnt[i]) * rightArea[i];
+                if (cost < bestCost) { bestCost = cost; axis = a; splitPos = cmin[a] + step * double(i + 1); }
+            }
+        }
+    }
+    void subdivide(int64_t nodeIdx) {                                     // :128-188
+        const int64_t primCount = B.count[nodeIdx];
+        if (primCount <= maxLeaf && nodeIdx != 0) return;
+        int bestAxis = 0; double bestPos = 0;
+        const int64_t first = B.leftFirst[nodeIdx];
+        findBestSplitPlane(first, primCount, bestAxis, bestPos);
+        int64_t i = first, j = i + primCount - 1;
+        while (i <= j) {
+            if (P.cen[3 * B.primIdx[i] + bestAxis] < bestPos) i += 1;
+            else { std::swap(B.primIdx[i], B.primIdx[j]); j -= 1; }
+        }
+        const int64_t leftCount = i - first;
+        if (leftCount == 0 || leftCount == primCount) return;
+        const int64_t leftChild = ++B.nodesUsed;
+        const int64_t rightChild = ++B.nodesUsed;
+        B.leftFirst[leftChild] = first; B.count[leftChild] = leftCount;
+        B.leftFirst[rightChild] = i; B.count[rightChild] = primCount - leftCount;
+        B.leftFirst[nodeIdx] = leftChild; B.count[nodeIdx] = 0;
+        updateNodeBounds(leftChild);
+        updateNodeBounds(rightChild);
+        subdivide(leftChild);
+        subdivide(rightChild);
+    }
+};
+}  // namespace
+
+RefBVH build_ref_bvh(const PrimSet& prims, int maxLeaf, int binCount) {
+    RefBVH B;
+    const int64_t n = prims.n;
+    const int64_t nodeCount = std::max<int64_t>(1, n * 2 - 1);
+    B.lo.assign(3 * nodeCount, 0.0); B.hi.assign(3 * nodeCount, 0.0);
+    B.leftFirst.assign(nodeCount, 0); B.count.assign(nodeCount, 0);
+    B.primIdx.resize(n);
+    for (int64_t i = 0; i < n; ++i) B.primIdx[i] = i;
+    B.leftFirst[0] = 0; B.count[0] = n; B.nodesUsed = 0;
+    Builder bld(prims, B, maxLeaf, binCount);
+    bld.updateNodeBounds(0);
+    bld.subdivide(0);
+    return B;
+}
+
+uint64_t ref_bvh_hash(const RefBVH& b, const std::vector<int64_t>& primIndexOf) {
+    // Same canonical walk as oracle_bvh_hash (tests compare the two).
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t x) { for (int i = 0; i < 8; ++i) { h ^= (x >> (8 * i)) & 0xff; h *= 1099511628211ull; } };
+    auto mixd = [&](double d) { uint64_t u; std::memcpy(&u, &d, 8); mix(u); };
+    std::vector<int64_t> st{0};
+    while (!st.empty()) {
+        int64_t i = st.back(); st.pop_back();
+        for (int k = 0; k < 3; ++k) mixd(b.lo[3 * i + k]);
+        for (int k = 0; k < 3; ++k) mixd(b.hi[3 * i + k]);
+        if (b.isLeaf(i)) {
+            mix(0xABCDull); mix((uint64_t)b.count[i]);
+            for (int64_t q = 0; q < b.count[i]; ++q) mix((uint64_t)primIndexOf[b.primIdx[b.leftFirst[i] + q]]);
+        } else {
+            mix(0x1234ull);
+            st.push_back(b.leftFirst[i] + 1);
+            st.push_back(b.leftFirst[i]);
+        }
+    }
+    return h;
+}
+
+int64_t ref_bvh_depth(const RefBVH& b) {
+    int64_t best = 0;
+    std::vector<std::pair<int64_t, int64_t>> st{{0, 0}};
+    while (!st.empty()) {
+        auto [i, d] = st.back(); st.pop_back();
+        if (b.isLeaf(i) || b.count[i] == 0 && b.leftFirst[i] == 0) { best = std::max(best, d); continue; }
+        st.push_back({b.leftFirst[i], d + 1});
+        st.push_back({b.leftFirst[i] + 1, d + 1});
+    }
+    return best;
+}
+
+// -------------------------------------------------------------- matrices
+static void m4_inverse(const double* m, double* out) {   // cofactor inverse (see oracle note)
+    double inv[16];
+    inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+    for (int i = 0; i < 16; ++i) out[i] = inv[i] / det;
+}
+static double m3_det_of4(const double* M) {   // simd_determinant of the upper 3x3 (col-major a[c*3+r])
+    double a[9];
+    for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) a[c * 3 + r] = M[c * 4 + r];
+    return a[0] * (a[4] * a[8] - a[7] * a[5]) - a[3] * (a[1] * a[8] - a[7] * a[2]) + a[6] * (a[1] * a[5] - a[4] * a[2]);
+}
+static void normal_matrix(const double* M, double* out) {   // normalTransformMatrix (RTContext.swift:23-31)
+    auto e = [&](int r, int c) { return M[c * 4 + r]; };
+    const double det = m3_det_of4(M);
+    double cof[3][3];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            int r1 = (r + 1) % 3, r2 = (r + 2) % 3, c1 = (c + 1) % 3, c2 = (c + 2) % 3;
+            cof[r][c] = e(r1, c1) * e(r2, c2) - e(r1, c2) * e(r2, c1);
+        }
+    double inv[9];   // inv (r,c) col-major
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) inv[c * 3 + r] = cof[c][r] / det;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) out[c * 3 + r] = inv[r * 3 + c];   // transpose
+}
+// AABB.transformed(by:) (AABB.swift:71-92)
+static void aabb_transformed(const double* lo, const double* hi, const double* M, double* olo, double* ohi) {
+    const D3 mn = d3(lo[0], lo[1], lo[2]), mx = d3(hi[0], hi[1], hi[2]);
+    const D3 cOld = 0.5 * (mn + mx);
+    const D3 eOld = 0.5 * (mx - mn);
+    D3 rc;
+    {
+        double o[3];
+        for (int r = 0; r < 3; ++r) {
+            double acc = M[0 * 4 + r] * cOld.x;
+            acc = M[1 * 4 + r] * cOld.y + acc;
+            acc = M[2 * 4 + r] * cOld.z + acc;
+            o[r] = acc;
+        }
+        rc = d3(o[0], o[1], o[2]);
+    }
+    const D3 cNew = rc + d3(M[12], M[13], M[14]);
+    double ar[9];
+    for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) ar[c * 3 + r] = std::fabs(M[c * 4 + r]);
+    const D3 eNew = d3(ar[0] * eOld.x + ar[3] * eOld.y + ar[6] * eOld.z,
+                       ar[1] * eOld.x + ar[4] * eOld.y + ar[7] * eOld.z,
+                       ar[2] * eOld.x + ar[5] * eOld.y + ar[8] * eOld.z);
+    const D3 a = cNew - eNew, b = cNew + eNew;
+    olo[0] = a.x; olo[1] = a.y; olo[2] = a.z;
+    ohi[0] = b.x; ohi[1] = b.y; ohi[2] = b.z;
+}
+
+// ------------------------------------------------------------ scene flattening
+namespace {
+struct Tri { D3 v0, v1, v2, e1, e2, n0, n1, n2; };
+struct BlasBuild {
+    std::vector<int64_t> triIndex;   // subset prims -> global triangle index
+    PrimSet prims;
+    RefBVH bvh;
+    bool smooth = false;
+    D3 motion{0, 0, 0};
+    uint64_t hash = 0;
+    int64_t depth = 0;
+    // filled by layout
+    int32_t root_ref = 0;
+    double root_lo[3], root_hi[3];
+};
+struct InstBuild { int blas; double M[16]; int material; D3 motion; double wlo[3], whi[3]; };
+}  // namespace
+
+// Lay one reference-form BVH out as WRec records.  Inner nodes get records in DFS
+// preorder (near-left first); each leaf's primitives become a contiguous run of
+// entries produced by `emit_leaf(first_prim_slot, count)` which returns the index of
+// the run's first entry.  Returns the root ref.
+template <class EmitLeaf>
+static int32_t layout_bvh(const RefBVH& b, std::vector<WRec>& recs, EmitLeaf emit_leaf) {
+    if (b.isLeaf(0) || (b.count[0] == 0 && b.nodesUsed == 0)) {
+        const int64_t first = emit_leaf(b.leftFirst[0], b.count[0]);
+        return ~(int32_t)first;
+    }
+    // assign record ids in preorder
+    std::vector<int64_t> recOf(b.leftFirst.size(), -1);
+    std::vector<int64_t> order;
+    std::vector<int64_t> st{0};
+    while (!st.empty()) {
+        int64_t i = st.back(); st.pop_back();
+        recOf[i] = (int64_t)recs.size() + (int64_t)order.size();
+        order.push_back(i);
+        const int64_t L = b.leftFirst[i], R = L + 1;
+        if (!b.isLeaf(R)) st.push_back(R);
+        if (!b.isLeaf(L)) st.push_back(L);
+    }
+    const int64_t base = (int64_t)recs.size();
+    recs.resize(base + order.size());
+    // leaves are emitted in DFS order of the traversal (left before right)
+    for (size_t q = 0; q < order.size(); ++q) {
+        const int64_t i = order[q];
+        WRec& r = recs[base + q];
+        std::memset(&r, 0, sizeof(WRec));
+        const int64_t ch[2] = {b.leftFirst[i], b.leftFirst[i] + 1};
+        for (int c = 0; c < 2; ++c) {
+            for (int k = 0; k < 3; ++k) { r.lo[c][k] = b.lo[3 * ch[c] + k]; r.hi[c][k] = b.hi[3 * ch[c] + k]; }
+        }
+    }
+    // leaf runs: walk preorder so runs are laid out in traversal order
+    std::vector<int64_t> st2{0};
+    while (!st2.empty()) {
+        int64_t i = st2.back(); st2.pop_back();
+        WRec& r = recs[recOf[i]];
+        const int64_t ch[2] = {b.leftFirst[i], b.leftFirst[i] + 1};
+        for (int c = 0; c < 2; ++c) {
+            if (b.isLeaf(ch[c])) {
+                const int64_t first = emit_leaf(b.leftFirst[ch[c]], b.count[ch[c]]);
+                r.ref[c] = ~(int32_t)first;
+            } else {
+                r.ref[c] = (int32_t)recOf[ch[c]];
+            }
+        }
+        if (!b.isLeaf(ch[1])) st2.push_back(ch[1]);
+        if (!b.isLeaf(ch[0])) st2.push_back(ch[0]);
+    }
+    return (int32_t)recOf[0];
+}
+
+int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err) {
+    auto t0 = std::chrono::steady_clock::now();
+    S.eps = d->intersection_test_epsilon;
+    S.shadow_eps = d->shadow_ray_epsilon;
+    S.background[0] = d->background_color.x; S.background[1] = d->background_color.y; S.background[2] = d->background_color.z;
+    S.ambient[0] = d->ambient_light.x; S.ambient[1] = d->ambient_light.y; S.ambient[2] = d->ambient_light.z;
+    S.max_depth = d->max_recursion_depth;
+    if (d->num_materials < 0 || (d->num_materials > 0 && !d->materials)) { err = "bad materials"; return RT_ERR_INVALID_ARG; }
+    for (int i = 0; i < d->num_materials; ++i) {
+        const rt_material& m = d->materials[i];
+        DMaterial dm{};
+        const rt_vec3* src[5] = {&m.ambient, &m.diffuse, &m.specular, &m.mirror, &m.absorption};
+        double* dst[5] = {dm.ambient, dm.diffuse, dm.specular, dm.mirror, dm.absorption};
+        for (int k = 0; k < 5; ++k) { dst[k][0] = src[k]->x; dst[k][1] = src[k]->y; dst[k][2] = src[k]->z; }
+        dm.phong = m.phong; dm.ior = m.ior; dm.absorption_index = m.absorption_index; dm.roughness = m.roughness;
+        dm.type = m.type;
+        if (m.type == RT_MAT_DIELECTRIC) S.has_dielectric = true;
+        S.mats.push_back(dm);
+    }
+    for (int i = 0; i < d->num_point_lights; ++i) {
+        DPointLight l{};
+        l.position[0] = d->point_lights[i].position.x; l.position[1] = d->point_lights[i].position.y; l.position[2] = d->point_lights[i].position.z;
+        l.intensity[0] = d->point_lights[i].intensity.x; l.intensity[1] = d->point_lights[i].intensity.y; l.intensity[2] = d->point_lights[i].intensity.z;
+        S.plights.push_back(l);
+    }
+    S.num_area_lights = d->num_area_lights;
+    for (int i = 0; i < d->num_cameras; ++i) S.cams.push_back(d->cameras[i]);
+
+    // ---- flatten objects (RTContext.swift:120-378)
+    std::vector<Tri> triangles;
+    std::vector<BlasBuild> blases;
+    std::vector<InstBuild> insts;
+    struct Base { int blas; int material; double M[16]; };
+    std::map<int, Base> instanceByID;
+    std::vector<int> meshOrder;
+    std::vector<const rt_object*> meshInstances;
+
+    auto singleTriBlas = [&](const rt_object& o) {
+        Tri t{};
+        t.v0 = of(o.v[0]); t.v1 = of(o.v[1]); t.v2 = of(o.v[2]);
+        t.e1 = t.v1 - t.v0; t.e2 = t.v2 - t.v0;
+        D3 n = normalize(cross(t.e1, t.e2));
+        t.n0 = t.n1 = t.n2 = n;
+        const int64_t gi = (int64_t)triangles.size();
+        triangles.push_back(t);
+        BlasBuild bb;
+        bb.smooth = false;
+        bb.motion = of(o.motion_blur);
+        bb.triIndex.push_back(gi);
+        bb.prims.n = 1;
+        const D3 mn = vmin(t.v0, vmin(t.v1, t.v2)), mx = vmax(t.v0, vmax(t.v1, t.v2));
+        const D3 c = ((t.v0 + t.v1) + t.v2) / 3.0;
+        bb.prims.bmin = {mn.x, mn.y, mn.z}; bb.prims.bmax = {mx.x, mx.y, mx.z}; bb.prims.cen = {c.x, c.y, c.z};
+        return bb;
+    };
+
+    for (int oi = 0; oi < d->num_objects; ++oi) {
+        const rt_object& o = d->objects[oi];
+        if (o.kind == RT_OBJ_SPHERE) { err = "spheres are not implemented on the GPU path yet"; S.n_spheres++; return RT_ERR_UNSUPPORTED; }
+        if (o.kind == RT_OBJ_PLANE) { err = "planes are not implemented on the GPU path yet"; S.n_planes++; return RT_ERR_UNSUPPORTED; }
+        if (o.kind == RT_OBJ_TRIANGLE) {                                      // RTContext.swift:193-235
+            S.n_tris++;
+            blases.push_back(singleTriBlas(o));
+            InstBuild ib{};
+            ib.blas = (int)blases.size() - 1;
+            std::memcpy(ib.M, o.transform, sizeof(ib.M));
+            ib.material = o.material_id; ib.motion = d3(0, 0, 0);
+            insts.push_back(ib);
+            continue;
+        }
+        if (o.kind == RT_OBJ_MESH_INSTANCE) { meshInstances.push_back(&o); continue; }
+        if (o.kind != RT_OBJ_MESH) { err = "unknown object kind"; return RT_ERR_INVALID_ARG; }
+        // ---- Mesh (RTContext.swift:242-377)
+        S.n_meshes++;
+        std::vector<double> plyPos, plyNrm; std::vector<float> plyUV; std::vector<int32_t> plyIdx;
+        const double* P; const int32_t* I; const double* Nn = nullptr; int64_t nPos, nIdx; int64_t off;
+        if (o.ply_path) {
+            std::string perr;
+            int rc = ply_load(o.ply_path, plyPos, plyNrm, plyUV, plyIdx, perr);
+            if (rc != RT_OK) {            // `try? PLYLoader.load` failing -> mesh skipped (RTContext.swift:255-261)
+                continue;
+            }
+            P = plyPos.data(); nPos = (int64_t)plyPos.size() / 3;
+            I = plyIdx.data(); nIdx = (int64_t)plyIdx.size();
+            Nn = plyNrm.empty() ? nullptr : plyNrm.data();
+            off = 0;
+        } else {
+            P = o.positions; nPos = o.num_positions; I = o.indices; nIdx = o.num_indices;
+            Nn = o.normals; off = o.indices_one_based ? 1 : 0;
+            if ((nPos > 0 && !P) || (nIdx > 0 && !I)) { err = "mesh arrays missing"; return RT_ERR_INVALID_ARG; }
+        }
+        const bool isSmooth = o.smooth != 0;
+        const int64_t triCount = nIdx / 3;
+        for (int64_t t = 0; t < 3 * triCount; ++t) {
+            const int64_t k = (int64_t)I[t] - off;
+            if (k < 0 || k >= nPos) { err = "mesh index out of range"; return RT_ERR_INVALID_ARG; }
+        }
+        auto pos = [&](int64_t k) { return d3(P[3 * k], P[3 * k + 1], P[3 * k + 2]); };
+        const int64_t start = (int64_t)triangles.size();
+        S.n_tris += triCount;
+        BlasBuild bb;
+        bb.smooth = isSmooth;
+        bb.motion = of(o.motion_blur);
+        const bool blur = !(bb.motion.x == 0 && bb.motion.y == 0 && bb.motion.z == 0);
+        bb.prims.n = triCount;
+        bb.prims.bmin.resize(3 * triCount); bb.prims.bmax.resize(3 * triCount); bb.prims.cen.resize(3 * triCount);
+        bb.triIndex.resize(triCount);
+        std::vector<D3> vtx;
+        std::vector<D3> faceN;
+        if (!Nn) {
+            faceN.resize(triCount);
+            for (int64_t t = 0; t < triCount; ++t) {
+                D3 v0 = pos(I[3 * t] - off), v1 = pos(I[3 * t + 1] - off), v2 = pos(I[3 * t + 2] - off);
+                faceN[t] = normalize(cross(v1 - v0, v2 - v0));
+            }
+            if (isSmooth) {
+                vtx.assign(nPos, d3(0, 0, 0));
+                for (int64_t t = 0; t < triCount; ++t)
+                    for (int k = 0; k < 3; ++k) vtx[I[3 * t + k] - off] = vtx[I[3 * t + k] - off] + faceN[t];
+                for (auto& v : vtx) v = normalize(v);
+            }
+        }
+        triangles.resize(start + triCount);
+        for (int64_t t = 0; t < triCount; ++t) {
+            const int64_t i0 = I[3 * t] - off, i1 = I[3 * t + 1] - off, i2 = I[3 * t + 2] - off;
+            Tri& tr = triangles[start + t];
+            tr.v0 = pos(i0); tr.v1 = pos(i1); tr.v2 = pos(i2);
+            tr.e1 = tr.v1 - tr.v0; tr.e2 = tr.v2 - tr.v0;
+            if (Nn) {
+                tr.n0 = d3(Nn[3 * i0], Nn[3 * i0 + 1], Nn[3 * i0 + 2]);
+                tr.n1 = d3(Nn[3 * i1], Nn[3 * i1 + 1], Nn[3 * i1 + 2]);
+                tr.n2 = d3(Nn[3 * i2], Nn[3 * i2 + 1], Nn[3 * i2 + 2]);
+            } else if (isSmooth) {
+                tr.n0 = vtx[i0]; tr.n1 = vtx[i1]; tr.n2 = vtx[i2];
+            } else {
+                D3 n = normalize(faceN[t]);
+                tr.n0 = tr.n1 = tr.n2 = n;
+            }
+            const D3 c = ((tr.v0 + tr.v1) + tr.v2) / 3.0;
+            D3 mn = vmin(tr.v0, vmin(tr.v1, tr.v2)), mx = vmax(tr.v0, vmax(tr.v1, tr.v2));
+            if (blur) {
+                const D3 b0 = tr.v0 + bb.motion, b1 = tr.v1 + bb.motion, b2 = tr.v2 + bb.motion;
+                mn = vmin(mn, vmin(b0, vmin(b1, b2)));
+                mx = vmax(mx, vmax(b0, vmax(b1, b2)));
+            }
+            bb.prims.bmin[3 * t] = mn.x; bb.prims.bmin[3 * t + 1] = mn.y; bb.prims.bmin[3 * t + 2] = mn.z;
+            bb.prims.bmax[3 * t] = mx.x; bb.prims.bmax[3 * t + 1] = mx.y; bb.prims.bmax[3 * t + 2] = mx.z;
+            bb.prims.cen[3 * t] = c.x; bb.prims.cen[3 * t + 1] = c.y; bb.prims.cen[3 * t + 2] = c.z;
+            bb.triIndex[t] = start + t;
+        }
+        if (std::find(meshOrder.begin(), meshOrder.end(), o.id) == meshOrder.end()) meshOrder.push_back(o.id);
+        if (triCount > 0) {
+            blases.push_back(std::move(bb));
+            Base base{};
+            base.blas = (int)blases.size() - 1; base.material = o.material_id;
+            std::memcpy(base.M, o.transform, sizeof(base.M));
+            instanceByID[o.id] = base;
+        } else {
+            instanceByID.erase(o.id);
+        }
+    }
+    // MeshInstance objects (RTContext.swift:384-401), then base meshes in scene order (:403-410, H11)
+    for (const rt_object* mi : meshInstances) {
+        auto it = instanceByID.find(mi->base_mesh_id);
+        if (it == instanceByID.end()) continue;
+        InstBuild ib{};
+        ib.blas = it->second.blas;
+        std::memcpy(ib.M, mi->transform, sizeof(ib.M));
+        ib.material = mi->material_id; ib.motion = of(mi->motion_blur);
+        insts.push_back(ib);
+        Base nb{}; nb.blas = it->second.blas; nb.material = mi->material_id; std::memcpy(nb.M, mi->transform, sizeof(nb.M));
+        instanceByID[mi->id] = nb;
+    }
+    for (int meshID : meshOrder) {
+        auto it = instanceByID.find(meshID);
+        if (it == instanceByID.end()) continue;
+        InstBuild ib{};
+        ib.blas = it->second.blas;
+        std::memcpy(ib.M, it->second.M, sizeof(ib.M));
+        ib.material = it->second.material; ib.motion = d3(0, 0, 0);
+        insts.push_back(ib);
+    }
+
+    // ---- BLAS builds (buildBLASForMesh: maxLeaf 2, SAH, 12 bins; RTContext.swift:430-435)
+    int64_t maxBlasDepth = 0;
+    for (auto& bb : blases) {
+        bb.bvh = build_ref_bvh(bb.prims, 2, 12);
+        bb.hash = ref_bvh_hash(bb.bvh, bb.triIndex);
+        bb.depth = ref_bvh_depth(bb.bvh);
+        maxBlasDepth = std::max(maxBlasDepth, bb.depth);
+    }
+
+    // ---- device layout: BLAS records + leaf-ordered triangles
+    for (auto& bb : blases) {
+        auto emit = [&](int64_t firstSlot, int64_t count) -> int64_t {
+            const int64_t first = (int64_t)S.tris.size();
+            for (int64_t q = 0; q < count; ++q) {
+                const int64_t g = bb.triIndex[bb.bvh.primIdx[firstSlot + q]];
+                const Tri& t = triangles[g];
+                TriRec r{};
+                r.v0[0] = t.v0.x; r.v0[1] = t.v0.y; r.v0[2] = t.v0.z;
+                r.e1[0] = t.e1.x; r.e1[1] = t.e1.y; r.e1[2] = t.e1.z;
+                r.e2[0] = t.e2.x; r.e2[1] = t.e2.y; r.e2[2] = t.e2.z;
+                r.last = (q == count - 1) ? 1 : 0;
+                r.prim = (int32_t)g;
+                S.tris.push_back(r);
+                const D3 ns[3] = {t.n0, t.n1, t.n2};
+                for (int k = 0; k < 3; ++k) { S.normals.push_back(ns[k].x); S.normals.push_back(ns[k].y); S.normals.push_back(ns[k].z); }
+            }
+            return first;
+        };
+        bb.root_ref = layout_bvh(bb.bvh, S.recs, emit);
+        for (int k = 0; k < 3; ++k) { bb.root_lo[k] = bb.bvh.lo[k]; bb.root_hi[k] = bb.bvh.hi[k]; }
+        bb.bvh = RefBVH();   // free host copy
+        bb.prims = PrimSet();
+    }
+    S.blas_records = (int64_t)S.recs.size();
+
+    // ---- instances (makeInstance, RTContext.swift:437-457) and TLAS (buildTLAS :459-474)
+    PrimSet tp;
+    tp.n = (int64_t)insts.size();
+    double wlo[3] = {kInf, kInf, kInf}, whi[3] = {-kInf, -kInf, -kInf};
+    for (size_t i = 0; i < insts.size(); ++i) {
+        InstBuild& ib = insts[i];
+        const BlasBuild& bb = blases[ib.blas];
+        // world bounds: union of every prim's transformed bounds
+        D3 mn = d3(kInf, kInf, kInf), mx = d3(-kInf, -kInf, -kInf);
+        for (size_t q = 0; q < bb.triIndex.size(); ++q) {
+            const Tri& t = triangles[bb.triIndex[q]];
+            D3 pmn = vmin(t.v0, vmin(t.v1, t.v2)), pmx = vmax(t.v0, vmax(t.v1, t.v2));
+            if (!(bb.motion.x == 0 && bb.motion.y == 0 && bb.motion.z == 0)) {
+                const D3 b0 = t.v0 + bb.motion, b1 = t.v1 + bb.motion, b2 = t.v2 + bb.motion;
+                pmn = vmin(pmn, vmin(b0, vmin(b1, b2)));
+                pmx = vmax(pmx, vmax(b0, vmax(b1, b2)));
+            }
+            double lo[3] = {pmn.x, pmn.y, pmn.z}, hi[3] = {pmx.x, pmx.y, pmx.z}, olo[3], ohi[3];
+            aabb_transformed(lo, hi, ib.M, olo, ohi);
+            mn = vmin(mn, d3(olo[0], olo[1], olo[2]));
+            mx = vmax(mx, d3(ohi[0], ohi[1], ohi[2]));
+        }
+        ib.wlo[0] = mn.x; ib.wlo[1] = mn.y; ib.wlo[2] = mn.z;
+        ib.whi[0] = mx.x; ib.whi[1] = mx.y; ib.whi[2] = mx.z;
+        for (int k = 0; k < 3; ++k) { wlo[k] = std::fmin(wlo[k], ib.wlo[k]); whi[k] = std::fmax(whi[k], ib.whi[k]); }
+        tp.bmin.insert(tp.bmin.end(), ib.wlo, ib.wlo + 3);
+        tp.bmax.insert(tp.bmax.end(), ib.whi, ib.whi + 3);
+        const D3 c = (d3(ib.wlo[0], ib.wlo[1], ib.wlo[2]) + d3(ib.whi[0], ib.whi[1], ib.whi[2])) * 0.5;
+        tp.cen.insert(tp.cen.end(), {c.x, c.y, c.z});
+
+        DInstance di{};
+        std::memcpy(di.l2w, ib.M, sizeof(di.l2w));
+        m4_inverse(ib.M, di.w2l);
+        normal_matrix(ib.M, di.nmat);
+        di.motion[0] = ib.motion.x; di.motion[1] = ib.motion.y; di.motion[2] = ib.motion.z;
+        di.tri_motion[0] = bb.motion.x; di.tri_motion[1] = bb.motion.y; di.tri_motion[2] = bb.motion.z;
+        for (int k = 0; k < 3; ++k) { di.root_lo[k] = bb.root_lo[k]; di.root_hi[k] = bb.root_hi[k]; }
+        di.root_ref = bb.root_ref;
+        di.material = ib.material;
+        di.smooth = bb.smooth ? 1 : 0;
+        di.det_neg = m3_det_of4(ib.M) < 0.0 ? 1 : 0;
+        S.insts.push_back(di);
+        S.inst_bvh_hash.push_back(bb.hash);
+    }
+    if (!insts.empty()) {
+        RefBVH tb = build_ref_bvh(tp, 2, 12);
+        std::vector<int64_t> ident(tp.n);
+        for (int64_t i = 0; i < tp.n; ++i) ident[i] = i;
+        S.tlas_hash = ref_bvh_hash(tb, ident);
+        const int64_t tdepth = ref_bvh_depth(tb);
+        for (int k = 0; k < 3; ++k) { S.tlas_root_lo[k] = tb.lo[k]; S.tlas_root_hi[k] = tb.hi[k]; }
+        auto emit = [&](int64_t firstSlot, int64_t count) -> int64_t {
+            const int64_t first = (int64_t)S.tlas_leaf.size();
+            for (int64_t q = 0; q < count; ++q)
+                S.tlas_leaf.push_back(DTlasLeafEntry{(int32_t)tb.primIdx[firstSlot + q], (q == count - 1) ? 1 : 0});
+            return first;
+        };
+        S.tlas_root_ref = layout_bvh(tb, S.recs, emit);
+        S.tlas_records = (int64_t)S.recs.size() - S.blas_records;
+        S.has_tlas = true;
+        S.max_stack = (tdepth + 1) + (maxBlasDepth + 1) + 2;
+        const double dx = whi[0] - wlo[0], dy = whi[1] - wlo[1], dz = whi[2] - wlo[2];
+        S.scene_extent = std::sqrt(dx * dx + dy * dy + dz * dz);
+        if (!std::isfinite(S.scene_extent) || S.scene_extent <= 0) S.scene_extent = 1.0;
+    }
+    if (S.recs.size() >= (size_t)INT32_MAX || S.tris.size() >= (size_t)INT32_MAX) { err = "scene too large for int32 refs"; return RT_ERR_UNSUPPORTED; }
+    if (maxBlasDepth + 1 > 63) { err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550)"; return RT_ERR_STACK; }
+    S.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+}  // namespace myrt

@@ -1,0 +1,245 @@
+"""Python host mirror of the reference's public engine API.
+
+`RayTracerEngine` mirrors `RayTracerEngine` (RT/RayTracer.swift:25-228): it is built
+from a scene (init(from:data:) :30-49), answers `inspect` (:52-67) and renders one
+camera (`render`, :115-131) or all cameras (`render_all`, :70-102), returning
+`RenderResult`s with RGBA8 pixels (:186-195) and `RenderStats` (Models/RenderStats.swift).
+
+Every render goes through libmyrt.so's C ABI (include/rtcore.h) into the HIP kernels;
+there is no CPU fallback — if the library or a GPU is missing, construction fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _abi as A
+from .scene import Scene
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmyrt.so")
+_lib = None
+
+
+class RenderError(RuntimeError):
+    """Raised for a negative rtcore status (NSError equivalents, RayTracer.swift:121,141-154)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[{code}] {message}")
+        self.code = code
+
+
+def load_library() -> C.CDLL:
+    """Load the in-tree HIP library.  torch is imported first so the process has ONE HIP
+    runtime (libmyrt.so then binds to torch's libamdhip64.so.7 by SONAME)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RenderError(A.RT_ERR_NO_RENDERER,
+                          f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        import torch  # noqa: F401  (shared HIP runtime)
+    except Exception:  # pragma: no cover - torch is part of the image
+        pass
+    _lib = A.bind(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def _check(rc: int):
+    if rc != A.RT_OK:
+        msg = load_library().rt_last_error()
+        raise RenderError(rc, msg.decode() if msg else "")
+
+
+@dataclass
+class RenderStats:                       # Models/RenderStats.swift:8-24 (+ ray counts)
+    meshes: int
+    triangles: int
+    spheres: int
+    planes: int
+    rays: int                            # primary + shadow (the reference always reported 0)
+    primary_rays: int
+    shadow_rays: int
+    secondary_rays: int
+    milliseconds: float
+    kernel_ms: float
+
+
+@dataclass
+class CameraSpec:                        # Models/RenderConfig.swift:19-25
+    index: int
+    id: Optional[str]
+    image_name: Optional[str]
+    width: int
+    height: int
+
+
+@dataclass
+class SceneInfo:                         # Models/RenderConfig.swift:27-33
+    cameras: List[CameraSpec]
+    meshes: int
+    triangles: int
+    spheres: int
+    planes: int
+
+
+@dataclass
+class RenderResult:                      # Models/RenderResult.swift:10-15 (CGImage -> arrays)
+    file_name: Optional[str]
+    rgba8: np.ndarray                    # (H, W, 4) uint8, row 0 = top
+    rgb: np.ndarray                      # (H, W, 3) float64 — Renderer.render's [Vec3]
+    camera: CameraSpec
+    stats: RenderStats
+
+
+@dataclass
+class RenderProgress:                    # Models/RenderProgress.swift:8-14
+    fraction: float
+    message: Optional[str] = None
+
+
+class RayTracerEngine:
+    """Device-resident scene + renderer (one full replica per listed GPU)."""
+
+    def __init__(self, scene: Scene, devices: Optional[Sequence[int]] = None):
+        lib = load_library()
+        self.scene = scene
+        self._packed = scene.to_desc()
+        handle = C.c_void_p()
+        devs = list(devices) if devices else [0]
+        arr = (C.c_int32 * len(devs))(*devs)
+        _check(lib.rt_scene_create(self._packed.ptr, arr, len(devs), C.byref(handle)))
+        self._h = handle
+        self.devices = devs
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().rt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -- introspection (RayTracer.swift:52-67)
+    def info(self) -> A.rt_scene_info:
+        out = A.rt_scene_info()
+        _check(load_library().rt_scene_info_get(self._h, C.byref(out)))
+        return out
+
+    def camera_spec(self, index: int) -> CameraSpec:
+        c = self.scene.cameras[index]
+        return CameraSpec(index, c.id, c.image_name, int(c.image_resolution[0]), int(c.image_resolution[1]))
+
+    def inspect(self) -> SceneInfo:
+        i = self.info()
+        return SceneInfo([self.camera_spec(k) for k in range(len(self.scene.cameras))],
+                         int(i.meshes), int(i.triangles), int(i.spheres), int(i.planes))
+
+    # -- rendering
+    def render_rows(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
+                    want_rgba: bool = True, progress: Optional[Callable[[RenderProgress], bool]] = None):
+        """Render the selected 8-row chunks; returns (rgb[rows,W,3] f64, rgba[rows,W,4] u8, RenderStats)."""
+        lib = load_library()
+        if not (0 <= camera_index < len(self.scene.cameras)):
+            raise RenderError(A.RT_ERR_INVALID_CAMERA, "Invalid camera index")
+        cam = self.scene.cameras[camera_index]
+        W, H = max(1, int(cam.image_resolution[0])), max(1, int(cam.image_resolution[1]))
+        rows = lib.rt_rows_for_chunks(H, chunk_first, chunk_step)
+        rgb = np.empty((rows, W, 3), dtype=np.float64)
+        rgba = np.empty((rows, W, 4), dtype=np.uint8) if want_rgba else None
+        st = A.rt_stats()
+
+        def _cb(user, done, total):
+            if progress is None:
+                return 1
+            return 1 if progress(RenderProgress(done / max(total, 1), f"Row {done}/{total}")) else 0
+
+        cb = A.RT_PROGRESS_FN(_cb)
+        _check(lib.rt_render(self._h, camera_index, chunk_first, chunk_step,
+                             rgb.ctypes.data_as(A.c_double_p),
+                             rgba.ctypes.data_as(C.POINTER(C.c_uint8)) if rgba is not None else None,
+                             C.byref(st), cb, None))
+        stats = RenderStats(int(st.meshes), int(st.triangles), int(st.spheres), int(st.planes),
+                            int(st.primary_rays + st.shadow_rays), int(st.primary_rays), int(st.shadow_rays),
+                            int(st.secondary_rays), float(st.milliseconds), float(st.kernel_ms))
+        return rgb, rgba, stats
+
+    def render(self, camera_index: int = 0, progress: Optional[Callable[[RenderProgress], bool]] = None) -> RenderResult:
+        """RayTracerEngine.render(format:cameraIndex:progress:) (RayTracer.swift:115-131)."""
+        rgb, rgba, stats = self.render_rows(camera_index, 0, 1, True, progress)
+        spec = self.camera_spec(camera_index)
+        return RenderResult(self.scene.cameras[camera_index].image_name, rgba, rgb, spec, stats)
+
+    def render_all(self, progress: Optional[Callable[[RenderProgress], bool]] = None) -> List[RenderResult]:
+        """renderAll (RayTracer.swift:70-102)."""
+        return [self.render(k, progress) for k in range(len(self.scene.cameras))]
+
+    # -- device-resident path (bench / multi-GPU ranks)
+    def render_device(self, out_rgb_ptr: int, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
+                      slot: int = 0, stream: int = 0, out_rgba_ptr: int = 0):
+        """Enqueue a render into device buffers on `stream` (no host sync)."""
+        _check(load_library().rt_render_device(self._h, slot, camera_index, chunk_first, chunk_step,
+                                               C.c_void_p(out_rgb_ptr), C.c_void_p(out_rgba_ptr or None),
+                                               C.c_void_p(stream or None)))
+
+    def collect_stats(self, slot: int = 0) -> A.rt_stats:
+        st = A.rt_stats()
+        _check(load_library().rt_stats_collect(self._h, slot, C.byref(st)))
+        return st
+
+    def work_counters(self, out_rgb_ptr: int, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
+                      slot: int = 0, stream: int = 0) -> A.rt_work_counters:
+        wc = A.rt_work_counters()
+        _check(load_library().rt_render_device_counted(self._h, slot, camera_index, chunk_first, chunk_step,
+                                                       C.c_void_p(out_rgb_ptr), C.c_void_p(stream or None),
+                                                       C.byref(wc)))
+        return wc
+
+    def bvh_hash(self, instance: int) -> int:
+        return int(load_library().rt_debug_bvh_hash(self._h, instance))
+
+
+def rows_for_chunks(height: int, chunk_first: int, chunk_step: int) -> int:
+    """Pure-Python restatement of rt_rows_for_chunks (used by host-side sharding logic)."""
+    height = max(1, height)
+    n = (height + 7) // 8
+    return sum(min(8, height - 8 * c) for c in range(chunk_first, n, chunk_step)) if chunk_step >= 1 else 0
+
+
+def ply_load(path: str):
+    """PLYLoader.load (PLYReader.swift:54-210) through the product's C ABI.
+    Returns dict(positions (V,3) f64, normals (V,3) f64 | None, texcoords (V,2) f32 | None, indices (T,3) i32)."""
+    lib = load_library()
+    m = A.rt_ply_mesh()
+    _check(lib.rt_ply_load(path.encode(), C.byref(m)))
+    try:
+        pos = np.ctypeslib.as_array(m.positions, shape=(m.num_positions * 3,)).reshape(-1, 3).copy() \
+            if m.num_positions else np.zeros((0, 3))
+        nrm = np.ctypeslib.as_array(m.normals, shape=(m.num_normals * 3,)).reshape(-1, 3).copy() \
+            if m.num_normals else None
+        uv = np.ctypeslib.as_array(m.texcoords, shape=(m.num_texcoords * 2,)).reshape(-1, 2).copy() \
+            if m.num_texcoords else None
+        idx = np.ctypeslib.as_array(m.indices, shape=(m.num_indices,)).copy() if m.num_indices else \
+            np.zeros((0,), np.int32)
+    finally:
+        lib.rt_ply_free(C.byref(m))
+    return {"positions": pos, "normals": nrm, "texcoords": uv, "indices": idx.reshape(-1, 3) if idx.size % 3 == 0 else idx}

@@ -1,0 +1,27 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _built():
+    """Build the in-tree libraries once (no-op when up to date)."""
+    from myraytracer_amd import build as B
+    B.build_product()
+    B.build_oracle()
+    yield
+
+
+@pytest.fixture(scope="session")
+def scene_dir(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("scenes"))

@@ -1,0 +1,22 @@
+#!/usr/bin/env bash
+# Run a sequence of GPU steps on the gpurun box.  Each step has its own time limit;
+# the session stops at the first fault-like exit (timeout 124/137, abort 134, segv 139,
+# or a signal) and continues past ordinary failures (exit 1 = test failures).
+# usage: tools/gpu_session.sh "<name>|<seconds>|<command>" ...
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for spec in "$@"; do
+  name="${spec%%|*}"; rest="${spec#*|}"; secs="${rest%%|*}"; cmd="${rest#*|}"
+  echo "=== [$name] (limit ${secs}s) $cmd" | tee -a gpurun_out/session.log
+  start=$(date +%s)
+  timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
+  rc=$?
+  echo "=== [$name] rc=$rc in $(( $(date +%s) - start ))s" | tee -a gpurun_out/session.log
+  tail -n 25 "gpurun_out/$name.log"
+  case $rc in
+    0|1|2|5) ;;
+    *) echo "=== stopping session after rc=$rc" | tee -a gpurun_out/session.log; exit $rc ;;
+  esac
+done
