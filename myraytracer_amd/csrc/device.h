@@ -1,0 +1,346 @@
+// device.h — device-side building blocks shared by the megakernel (render.hip) and
+// the wavefront pipeline (wavefront.hip).  IEEE binary64 throughout; every function
+// restates a reference routine (file:line cited) in the same operation order.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "layout.h"
+
+namespace myrt {
+namespace dev {
+
+
+#define DINF __builtin_huge_val()
+
+struct V3 { double x, y, z; };
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 ld3(const double* p) { return V3{p[0], p[1], p[2]}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ V3 operator/(V3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ V3 operator+(double s, V3 a) { return {s + a.x, s + a.y, s + a.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, double s) { return {a.x - s, a.y - s, a.z - s}; }
+__device__ __forceinline__ V3 operator+(V3 a, double s) { return {a.x + s, a.y + s, a.z + s}; }
+__device__ __forceinline__ V3 rcp(V3 a) { return {1.0 / a.x, 1.0 / a.y, 1.0 / a.z}; }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ V3 normalize(V3 v) { double r = 1.0 / dsqrt(dot(v, v)); return v * r; }
+__device__ __forceinline__ double length(V3 v) { return dsqrt(dot(v, v)); }
+__device__ __forceinline__ double smax(double x, double y) { return (y >= x) ? y : x; }   // Swift.max
+__device__ __forceinline__ double smin(double x, double y) { return (y < x) ? y : x; }    // Swift.min
+__device__ __forceinline__ bool isfin(V3 v) {
+    return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
+}
+// simd_mul(double4x4, double4) without FMA: ((c0*x + c1*y) + c2*z) + c3*w
+__device__ __forceinline__ V3 m4_point(const double* M, V3 v, double w) {
+    double o[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        double acc = M[0 * 4 + r] * v.x;
+        acc = M[1 * 4 + r] * v.y + acc;
+        acc = M[2 * 4 + r] * v.z + acc;
+        acc = M[3 * 4 + r] * w + acc;
+        o[r] = acc;
+    }
+    return {o[0], o[1], o[2]};
+}
+__device__ __forceinline__ V3 m3_mul(const double* M, V3 v) {
+    double o[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        double acc = M[0 * 3 + r] * v.x;
+        acc = M[1 * 3 + r] * v.y + acc;
+        acc = M[2 * 3 + r] * v.z + acc;
+        o[r] = acc;
+    }
+    return {o[0], o[1], o[2]};
+}
+
+// hitAABB (RTContext.swift:557-565): simd.min/max = fmin/fmax, scalar max/min = Swift's
+__device__ __forceinline__ double slab(double lx, double ly, double lz, double hx, double hy, double hz,
+                                       const V3& o, const V3& inv, double eps) {
+    const double t1x = (lx - o.x) * inv.x, t1y = (ly - o.y) * inv.y, t1z = (lz - o.z) * inv.z;
+    const double t2x = (hx - o.x) * inv.x, t2y = (hy - o.y) * inv.y, t2z = (hz - o.z) * inv.z;
+    const double mnx = fmin(t1x, t2x), mny = fmin(t1y, t2y), mnz = fmin(t1z, t2z);
+    const double mxx = fmax(t1x, t2x), mxy = fmax(t1y, t2y), mxz = fmax(t1z, t2z);
+    const double tmin = smax(smax(mnx, mny), mnz);
+    const double tmax = smin(mxx, smin(mxy, mxz));
+    return (tmax >= smax(tmin, eps)) ? tmin : DINF;
+}
+
+// PCG32 (Object+Extension.swift:556-589)
+struct PCG32 {
+    unsigned long long state, inc;
+    __device__ explicit PCG32(unsigned long long seed) {
+        state = 0ull; inc = (seed << 1) | 1ull;
+        (void)next();
+        state += 0x9E3779B97F4A7C15ull;
+        (void)next();
+    }
+    __device__ __forceinline__ unsigned next() {
+        const unsigned long long old = state;
+        state = old * 6364136223846793005ull + inc;
+        const unsigned xs = (unsigned)(((old >> 18) ^ old) >> 27);
+        const unsigned rot = (unsigned)(old >> 59);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31u));
+    }
+    __device__ __forceinline__ double nextFloat() { return (double)next() * 2.3283064365386963e-10; }
+};
+
+// ----------------------------------------------------------------- traversal stack
+// Per-lane stack: the first kLds entries live in LDS ([slot][lane] so each lane hits
+// its own bank), deeper entries spill to a private array (scratch).  An entry is
+// {ref, entry distance rounded down to float} so far subtrees can be culled at pop.
+constexpr int kLds = 16;
+constexpr int kSpill = 64;
+// LDS-qualified pointer: a plain pointer is generic (flat) and every push/pop would
+// compile to flat_load/flat_store on the vector-memory path instead of ds_*.
+// An entry packs {ref (low 32 bits), entry distance as float bits (high 32 bits)}.
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+struct Stack {
+    lds_u64* lds;        // &lds_base[threadIdx.x]; stride blockDim.x
+    int stride;
+    unsigned long long spill[kSpill];
+    int sp;
+    // The empty asm in the rare spill branch keeps the compiler from merging the two
+    // accesses into one select-of-pointers (which would force a generic flat access).
+    __device__ __forceinline__ void push(int ref, float t) {
+        const unsigned long long e = (unsigned long long)(unsigned)ref |
+                                     ((unsigned long long)(unsigned)__float_as_int(t) << 32);
+        if (sp < kLds) {
+            lds[sp * stride] = e;
+        } else {
+            asm volatile("" ::: "memory");
+            spill[sp - kLds] = e;
+        }
+        ++sp;
+    }
+    __device__ __forceinline__ int2 pop() {
+        --sp;
+        // unconditional ds_read of the clamped slot; the spill load only overrides it
+        unsigned long long e = lds[min(sp, kLds - 1) * stride];
+        if (sp >= kLds) {
+            asm volatile("" ::: "memory");
+            e = spill[sp - kLds];
+        }
+        return make_int2((int)(unsigned)(e & 0xffffffffull), (int)(unsigned)(e >> 32));
+    }
+};
+
+struct Counts { unsigned shadow, secondary; unsigned long long recs, tris, normals, insts; };
+
+struct Hit { double t, u, v; int tri, inst; };
+
+__device__ __forceinline__ float round_down_f(double d) { return __double2float_rd(d); }
+
+// Closest-hit triangle test, intersectTriangle (RTContext.swift:479-510) minus the
+// hit-point/normal writes, which are recomputed once for the final hit (same values).
+__device__ __forceinline__ void tri_closest(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double eps,
+                                           Hit& h, int triIdx, int instIdx) {
+    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+    const V3 pvec = cross(d, e2);
+    const double det = dot(e1, pvec);
+    if (fabs(det) < eps) return;
+    const double invDet = 1.0 / det;
+    const V3 tvec = o_mb - v0;
+    const double u = dot(tvec, pvec) * invDet;
+    if (u < 0.0 || u > 1.0) return;
+    const V3 q = cross(tvec, e1);
+    const double v = dot(d, q) * invDet;
+    if (v < 0.0 || u + v > 1.0) return;
+    const double t = dot(e2, q) * invDet;
+    if (t <= smax(eps, tlo) || t >= h.t) return;
+    h.t = t; h.u = u; h.v = v; h.tri = triIdx; h.inst = instIdx;
+}
+// triShadowHit (RTContext.swift:832-848)
+__device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double thi,
+                                           double eps) {
+    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+    const V3 pvec = cross(d, e2);
+    const double det = dot(e1, pvec);
+    if (fabs(det) < eps) return false;
+    const double invDet = 1.0 / det;
+    const V3 tvec = o_mb - v0;
+    const double u = dot(tvec, pvec) * invDet;
+    if (u < 0.0 || u > 1.0) return false;
+    const V3 q = cross(tvec, e1);
+    const double v = dot(d, q) * invDet;
+    if (v < 0.0 || u + v > 1.0) return false;
+    const double t = dot(e2, q) * invDet;
+    return (t > smax(eps, tlo) && t < thi);
+}
+
+// One ordered BVH walk shared by the closest-hit and any-hit queries.  `ref` is a
+// node the caller has already tested (the root); children are tested at the parent
+// (one 128-B record holds both), near pushed last (RTContext.swift:600-606).
+// LEAF(ref) handles a leaf run and returns true to terminate the walk (any-hit).
+// LIMIT() gives the current pruning distance.
+template <bool COUNT, class Leaf, class Limit>
+__device__ __forceinline__ bool walk(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st, int base,
+                                     Counts& c, Leaf leaf, Limit limit) {
+    const double eps = P.eps;
+    for (;;) {
+        if (ref >= 0) {
+            const WRec& R = P.recs[ref];
+            if (COUNT) c.recs++;
+            double d0 = slab(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv, eps);
+            double d1 = slab(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv, eps);
+            const double lim = limit();
+            if (d0 > lim) d0 = DINF;
+            if (d1 > lim) d1 = DINF;
+            int a = R.ref[0], b = R.ref[1];
+            if (d0 > d1) { const double td = d0; d0 = d1; d1 = td; const int tr = a; a = b; b = tr; }
+            if (d0 != DINF) {
+                if (d1 != DINF) st.push(b, round_down_f(d1));
+                ref = a;
+                continue;
+            }
+        } else {
+            if (leaf(ref)) return true;
+        }
+        // pop, culling entries that start beyond the current limit
+        for (;;) {
+            if (st.sp == base) return false;
+            const int2 e = st.pop();
+            if ((double)__int_as_float(e.y) > limit()) continue;
+            ref = e.x;
+            break;
+        }
+    }
+}
+
+template <bool COUNT>
+__device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
+                                  double time, Hit& h, Stack& st, Counts& c) {
+    const double eps = P.eps;
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    auto limit = [&]() { return h.t * P.prune_rel + P.prune_abs; };   // prune_rel = 1 + delta
+    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
+                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
+    if (d0 == DINF) return;
+    auto tlas_leaf = [&](int ref) -> bool {
+        for (int e = ~ref;; ++e) {
+            const DTlasLeafEntry le = P.tlas_leaf[e];
+            const DInstance& I = P.insts[le.inst];
+            if (COUNT) c.insts++;
+            // world -> local (RTContext.swift:657-673)
+            const V3 instOffset = ld3(I.motion) * time;
+            const V3 ow = o - instOffset;
+            const V3 ol = m4_point(I.w2l, ow, 1.0);
+            const V3 dl = m4_point(I.w2l, d, 0.0);
+            const V3 il = rcp(dl);
+            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                                   I.root_hi[2], ol, il, eps);
+            if (dr != DINF && !(dr > limit())) {
+                const V3 omb = ol - ld3(I.tri_motion) * time;   // Triangle.motionBlur offset (:480-481)
+                const int inst = le.inst;
+                auto blas_leaf = [&](int r) -> bool {
+                    for (int t = ~r;; ++t) {
+                        const TriRec& T = P.tris[t];
+                        if (COUNT) c.tris++;
+                        tri_closest(T, omb, dl, tlo, eps, h, t, inst);
+                        if (T.last) break;
+                    }
+                    return false;
+                };
+                const int sbase = st.sp;
+                if (I.root_ref < 0) blas_leaf(I.root_ref);
+                else walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+            }
+            if (le.last) break;
+        }
+        return false;
+    };
+    const int base = st.sp;
+    if (P.tlas_root_ref < 0) tlas_leaf(P.tlas_root_ref);
+    else walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+}
+
+template <bool COUNT>
+__device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time, Stack& st,
+                         Counts& c) {
+    if (!P.has_tlas) return false;
+    const double eps = P.eps;
+    const V3 inv = rcp(d);
+    const double lim = tmax * P.prune_rel + P.prune_abs;
+    auto limit = [&]() { return lim; };
+    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
+                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
+    if (d0 == DINF || d0 > lim) return false;
+    auto tlas_leaf = [&](int ref) -> bool {
+        for (int e = ~ref;; ++e) {
+            const DTlasLeafEntry le = P.tlas_leaf[e];
+            const DInstance& I = P.insts[le.inst];
+            if (COUNT) c.insts++;
+            const V3 instOffset = ld3(I.motion) * time;
+            const V3 ol = m4_point(I.w2l, o - instOffset, 1.0);
+            const V3 dl = m4_point(I.w2l, d, 0.0);
+            const V3 il = rcp(dl);
+            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                                   I.root_hi[2], ol, il, eps);
+            if (dr != DINF && !(dr > lim)) {
+                const V3 omb = ol - ld3(I.tri_motion) * time;
+                auto blas_leaf = [&](int r) -> bool {
+                    for (int t = ~r;; ++t) {
+                        const TriRec& T = P.tris[t];
+                        if (COUNT) c.tris++;
+                        if (tri_shadow(T, omb, dl, 0.0, tmax, eps)) return true;
+                        if (T.last) break;
+                    }
+                    return false;
+                };
+                const int sbase = st.sp;
+                bool hit;
+                if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
+                else hit = walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+                if (hit) { st.sp = sbase; return true; }
+            }
+            if (le.last) break;
+        }
+        return false;
+    };
+    const int base = st.sp;
+    bool hit;
+    if (P.tlas_root_ref < 0) hit = tlas_leaf(P.tlas_root_ref);
+    else hit = walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+    st.sp = base;
+    return hit;
+}
+
+// orthonormalBasis (Object+Extension.swift:531-552)
+__device__ __forceinline__ void onb(V3 n, V3& tangent, V3& bitangent) {
+    const double sign = n.z >= 0 ? 1.0 : -1.0;
+    const double a = -1.0 / (sign + n.z);
+    const double b = (n.x * n.y) * a;
+    tangent = normalize(v3(1.0 + ((sign * n.x) * n.x) * a, sign * b, (-sign) * n.x));
+    bitangent = normalize(v3(b, sign + (n.y * n.y) * a, -n.y));
+}
+__device__ __forceinline__ V3 reflect(V3 d, V3 n) { return d - (2.0 * dot(d, n)) * n; }
+// fresnelConductorRGB (Object+Extension.swift:493-505)
+__device__ __forceinline__ V3 fresnel_conductor(double eta, double k, double cosI_) {
+    const double cosI = smax(0.0, smin(1.0, fabs(cosI_)));
+    const double cos2 = cosI * cosI;
+    const double eta2k2 = eta * eta + k * k;
+    const double twoEtaCos = (2.0 * eta) * cosI;
+    const V3 cos2v = v3(cos2, cos2, cos2), one = v3(1, 1, 1);
+    const V3 Rs = ((eta2k2 - twoEtaCos) + cos2v) / ((eta2k2 + twoEtaCos) + cos2v);
+    const V3 Rp = (((eta2k2 * cos2v) - twoEtaCos) + one) / (((eta2k2 * cos2v) + twoEtaCos) + one);
+    return 0.5 * (Rs + Rp);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+}  // namespace dev
+}  // namespace myrt

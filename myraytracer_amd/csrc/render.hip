@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -25,320 +26,13 @@
 #include <vector>
 
 #include "../../include/rtcore.h"
+#include "device.h"
 #include "layout.h"
 #include "scene.h"
+#include "wavefront.h"
 
 namespace myrt {
 namespace dev {
-
-#define DINF __builtin_huge_val()
-
-struct V3 { double x, y, z; };
-__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 ld3(const double* p) { return V3{p[0], p[1], p[2]}; }
-__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
-__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
-__device__ __forceinline__ V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
-__device__ __forceinline__ V3 operator*(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
-__device__ __forceinline__ V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
-__device__ __forceinline__ V3 operator/(V3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
-__device__ __forceinline__ V3 operator+(double s, V3 a) { return {s + a.x, s + a.y, s + a.z}; }
-__device__ __forceinline__ V3 operator-(V3 a, double s) { return {a.x - s, a.y - s, a.z - s}; }
-__device__ __forceinline__ V3 operator+(V3 a, double s) { return {a.x + s, a.y + s, a.z + s}; }
-__device__ __forceinline__ V3 rcp(V3 a) { return {1.0 / a.x, 1.0 / a.y, 1.0 / a.z}; }
-__device__ __forceinline__ double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
-__device__ __forceinline__ V3 cross(V3 a, V3 b) {
-    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
-}
-__device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
-__device__ __forceinline__ V3 normalize(V3 v) { double r = 1.0 / dsqrt(dot(v, v)); return v * r; }
-__device__ __forceinline__ double length(V3 v) { return dsqrt(dot(v, v)); }
-__device__ __forceinline__ double smax(double x, double y) { return (y >= x) ? y : x; }   // Swift.max
-__device__ __forceinline__ double smin(double x, double y) { return (y < x) ? y : x; }    // Swift.min
-__device__ __forceinline__ bool isfin(V3 v) {
-    return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
-}
-// simd_mul(double4x4, double4) without FMA: ((c0*x + c1*y) + c2*z) + c3*w
-__device__ __forceinline__ V3 m4_point(const double* M, V3 v, double w) {
-    double o[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        double acc = M[0 * 4 + r] * v.x;
-        acc = M[1 * 4 + r] * v.y + acc;
-        acc = M[2 * 4 + r] * v.z + acc;
-        acc = M[3 * 4 + r] * w + acc;
-        o[r] = acc;
-    }
-    return {o[0], o[1], o[2]};
-}
-__device__ __forceinline__ V3 m3_mul(const double* M, V3 v) {
-    double o[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        double acc = M[0 * 3 + r] * v.x;
-        acc = M[1 * 3 + r] * v.y + acc;
-        acc = M[2 * 3 + r] * v.z + acc;
-        o[r] = acc;
-    }
-    return {o[0], o[1], o[2]};
-}
-
-// hitAABB (RTContext.swift:557-565): simd.min/max = fmin/fmax, scalar max/min = Swift's
-__device__ __forceinline__ double slab(double lx, double ly, double lz, double hx, double hy, double hz,
-                                       const V3& o, const V3& inv, double eps) {
-    const double t1x = (lx - o.x) * inv.x, t1y = (ly - o.y) * inv.y, t1z = (lz - o.z) * inv.z;
-    const double t2x = (hx - o.x) * inv.x, t2y = (hy - o.y) * inv.y, t2z = (hz - o.z) * inv.z;
-    const double mnx = fmin(t1x, t2x), mny = fmin(t1y, t2y), mnz = fmin(t1z, t2z);
-    const double mxx = fmax(t1x, t2x), mxy = fmax(t1y, t2y), mxz = fmax(t1z, t2z);
-    const double tmin = smax(smax(mnx, mny), mnz);
-    const double tmax = smin(mxx, smin(mxy, mxz));
-    return (tmax >= smax(tmin, eps)) ? tmin : DINF;
-}
-
-// PCG32 (Object+Extension.swift:556-589)
-struct PCG32 {
-    unsigned long long state, inc;
-    __device__ explicit PCG32(unsigned long long seed) {
-        state = 0ull; inc = (seed << 1) | 1ull;
-        (void)next();
-        state += 0x9E3779B97F4A7C15ull;
-        (void)next();
-    }
-    __device__ __forceinline__ unsigned next() {
-        const unsigned long long old = state;
-        state = old * 6364136223846793005ull + inc;
-        const unsigned xs = (unsigned)(((old >> 18) ^ old) >> 27);
-        const unsigned rot = (unsigned)(old >> 59);
-        return (xs >> rot) | (xs << ((~rot + 1u) & 31u));
-    }
-    __device__ __forceinline__ double nextFloat() { return (double)next() * 2.3283064365386963e-10; }
-};
-
-// ----------------------------------------------------------------- traversal stack
-// Per-lane stack: the first kLds entries live in LDS ([slot][lane] so each lane hits
-// its own bank), deeper entries spill to a private array (scratch).  An entry is
-// {ref, entry distance rounded down to float} so far subtrees can be culled at pop.
-constexpr int kLds = 16;
-constexpr int kSpill = 64;
-struct Stack {
-    int2* lds;           // &lds_base[threadIdx.x]; stride blockDim.x
-    int stride;
-    int2 spill[kSpill];
-    int sp;
-    __device__ __forceinline__ void push(int ref, float t) {
-        const int2 e = make_int2(ref, __float_as_int(t));
-        if (sp < kLds) lds[sp * stride] = e; else spill[sp - kLds] = e;
-        ++sp;
-    }
-    __device__ __forceinline__ int2 pop() {
-        --sp;
-        return (sp < kLds) ? lds[sp * stride] : spill[sp - kLds];
-    }
-};
-
-struct Counts { unsigned shadow, secondary; unsigned long long recs, tris, normals, insts; };
-
-struct Hit { double t, u, v; int tri, inst; };
-
-__device__ __forceinline__ float round_down_f(double d) { return __double2float_rd(d); }
-
-// Closest-hit triangle test, intersectTriangle (RTContext.swift:479-510) minus the
-// hit-point/normal writes, which are recomputed once for the final hit (same values).
-__device__ __forceinline__ void tri_closest(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double eps,
-                                           Hit& h, int triIdx, int instIdx) {
-    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
-    const V3 pvec = cross(d, e2);
-    const double det = dot(e1, pvec);
-    if (fabs(det) < eps) return;
-    const double invDet = 1.0 / det;
-    const V3 tvec = o_mb - v0;
-    const double u = dot(tvec, pvec) * invDet;
-    if (u < 0.0 || u > 1.0) return;
-    const V3 q = cross(tvec, e1);
-    const double v = dot(d, q) * invDet;
-    if (v < 0.0 || u + v > 1.0) return;
-    const double t = dot(e2, q) * invDet;
-    if (t <= smax(eps, tlo) || t >= h.t) return;
-    h.t = t; h.u = u; h.v = v; h.tri = triIdx; h.inst = instIdx;
-}
-// triShadowHit (RTContext.swift:832-848)
-__device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double thi,
-                                           double eps) {
-    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
-    const V3 pvec = cross(d, e2);
-    const double det = dot(e1, pvec);
-    if (fabs(det) < eps) return false;
-    const double invDet = 1.0 / det;
-    const V3 tvec = o_mb - v0;
-    const double u = dot(tvec, pvec) * invDet;
-    if (u < 0.0 || u > 1.0) return false;
-    const V3 q = cross(tvec, e1);
-    const double v = dot(d, q) * invDet;
-    if (v < 0.0 || u + v > 1.0) return false;
-    const double t = dot(e2, q) * invDet;
-    return (t > smax(eps, tlo) && t < thi);
-}
-
-// One ordered BVH walk shared by the closest-hit and any-hit queries.  `ref` is a
-// node the caller has already tested (the root); children are tested at the parent
-// (one 128-B record holds both), near pushed last (RTContext.swift:600-606).
-// LEAF(ref) handles a leaf run and returns true to terminate the walk (any-hit).
-// LIMIT() gives the current pruning distance.
-template <bool COUNT, class Leaf, class Limit>
-__device__ __forceinline__ bool walk(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st, int base,
-                                     Counts& c, Leaf leaf, Limit limit) {
-    const double eps = P.eps;
-    for (;;) {
-        if (ref >= 0) {
-            const WRec& R = P.recs[ref];
-            if (COUNT) c.recs++;
-            double d0 = slab(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv, eps);
-            double d1 = slab(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv, eps);
-            const double lim = limit();
-            if (d0 > lim) d0 = DINF;
-            if (d1 > lim) d1 = DINF;
-            int a = R.ref[0], b = R.ref[1];
-            if (d0 > d1) { const double td = d0; d0 = d1; d1 = td; const int tr = a; a = b; b = tr; }
-            if (d0 != DINF) {
-                if (d1 != DINF) st.push(b, round_down_f(d1));
-                ref = a;
-                continue;
-            }
-        } else {
-            if (leaf(ref)) return true;
-        }
-        // pop, culling entries that start beyond the current limit
-        for (;;) {
-            if (st.sp == base) return false;
-            const int2 e = st.pop();
-            if ((double)__int_as_float(e.y) > limit()) continue;
-            ref = e.x;
-            break;
-        }
-    }
-}
-
-template <bool COUNT>
-__device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
-                                  double time, Hit& h, Stack& st, Counts& c) {
-    const double eps = P.eps;
-    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-    auto limit = [&]() { return h.t * P.prune_rel + P.prune_abs; };   // prune_rel = 1 + delta
-    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
-                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
-    if (d0 == DINF) return;
-    auto tlas_leaf = [&](int ref) -> bool {
-        for (int e = ~ref;; ++e) {
-            const DTlasLeafEntry le = P.tlas_leaf[e];
-            const DInstance& I = P.insts[le.inst];
-            if (COUNT) c.insts++;
-            // world -> local (RTContext.swift:657-673)
-            const V3 instOffset = ld3(I.motion) * time;
-            const V3 ow = o - instOffset;
-            const V3 ol = m4_point(I.w2l, ow, 1.0);
-            const V3 dl = m4_point(I.w2l, d, 0.0);
-            const V3 il = rcp(dl);
-            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
-                                   I.root_hi[2], ol, il, eps);
-            if (dr != DINF && !(dr > limit())) {
-                const V3 omb = ol - ld3(I.tri_motion) * time;   // Triangle.motionBlur offset (:480-481)
-                const int inst = le.inst;
-                auto blas_leaf = [&](int r) -> bool {
-                    for (int t = ~r;; ++t) {
-                        const TriRec& T = P.tris[t];
-                        if (COUNT) c.tris++;
-                        tri_closest(T, omb, dl, tlo, eps, h, t, inst);
-                        if (T.last) break;
-                    }
-                    return false;
-                };
-                const int sbase = st.sp;
-                if (I.root_ref < 0) blas_leaf(I.root_ref);
-                else walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
-            }
-            if (le.last) break;
-        }
-        return false;
-    };
-    const int base = st.sp;
-    if (P.tlas_root_ref < 0) tlas_leaf(P.tlas_root_ref);
-    else walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
-}
-
-template <bool COUNT>
-__device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time, Stack& st,
-                         Counts& c) {
-    if (!P.has_tlas) return false;
-    const double eps = P.eps;
-    const V3 inv = rcp(d);
-    const double lim = tmax * P.prune_rel + P.prune_abs;
-    auto limit = [&]() { return lim; };
-    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
-                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
-    if (d0 == DINF || d0 > lim) return false;
-    auto tlas_leaf = [&](int ref) -> bool {
-        for (int e = ~ref;; ++e) {
-            const DTlasLeafEntry le = P.tlas_leaf[e];
-            const DInstance& I = P.insts[le.inst];
-            if (COUNT) c.insts++;
-            const V3 instOffset = ld3(I.motion) * time;
-            const V3 ol = m4_point(I.w2l, o - instOffset, 1.0);
-            const V3 dl = m4_point(I.w2l, d, 0.0);
-            const V3 il = rcp(dl);
-            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
-                                   I.root_hi[2], ol, il, eps);
-            if (dr != DINF && !(dr > lim)) {
-                const V3 omb = ol - ld3(I.tri_motion) * time;
-                auto blas_leaf = [&](int r) -> bool {
-                    for (int t = ~r;; ++t) {
-                        const TriRec& T = P.tris[t];
-                        if (COUNT) c.tris++;
-                        if (tri_shadow(T, omb, dl, 0.0, tmax, eps)) return true;
-                        if (T.last) break;
-                    }
-                    return false;
-                };
-                const int sbase = st.sp;
-                bool hit;
-                if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
-                else hit = walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
-                if (hit) { st.sp = sbase; return true; }
-            }
-            if (le.last) break;
-        }
-        return false;
-    };
-    const int base = st.sp;
-    bool hit;
-    if (P.tlas_root_ref < 0) hit = tlas_leaf(P.tlas_root_ref);
-    else hit = walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
-    st.sp = base;
-    return hit;
-}
-
-// orthonormalBasis (Object+Extension.swift:531-552)
-__device__ __forceinline__ void onb(V3 n, V3& tangent, V3& bitangent) {
-    const double sign = n.z >= 0 ? 1.0 : -1.0;
-    const double a = -1.0 / (sign + n.z);
-    const double b = (n.x * n.y) * a;
-    tangent = normalize(v3(1.0 + ((sign * n.x) * n.x) * a, sign * b, (-sign) * n.x));
-    bitangent = normalize(v3(b, sign + (n.y * n.y) * a, -n.y));
-}
-__device__ __forceinline__ V3 reflect(V3 d, V3 n) { return d - (2.0 * dot(d, n)) * n; }
-// fresnelConductorRGB (Object+Extension.swift:493-505)
-__device__ __forceinline__ V3 fresnel_conductor(double eta, double k, double cosI_) {
-    const double cosI = smax(0.0, smin(1.0, fabs(cosI_)));
-    const double cos2 = cosI * cosI;
-    const double eta2k2 = eta * eta + k * k;
-    const double twoEtaCos = (2.0 * eta) * cosI;
-    const V3 cos2v = v3(cos2, cos2, cos2), one = v3(1, 1, 1);
-    const V3 Rs = ((eta2k2 - twoEtaCos) + cos2v) / ((eta2k2 + twoEtaCos) + cos2v);
-    const V3 Rp = (((eta2k2 * cos2v) - twoEtaCos) + one) / (((eta2k2 * cos2v) + twoEtaCos) + one);
-    return 0.5 * (Rs + Rp);
-}
-
 // trace() (Object+Extension.swift:96-283) for diffuse/mirror/conductor materials and
 // point lights.  The recursion Lo + M*trace(depth+1) is run forward and combined
 // backward with the same per-level NaN guard, so the result is the recursive one.
@@ -439,16 +133,11 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
     return L;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    return x;
-}
 
 // One block = 256 lanes = 4 waves; each wave renders an 8x8 tile of one 8-row chunk.
 template <bool COUNT, bool BOUNCE>
 __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
-    extern __shared__ int2 lds_stack[];
+    extern __shared__ unsigned long long lds_stack[];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int i = blockIdx.x * 32 + wave * 8 + (lane & 7);
@@ -461,7 +150,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     Counts cnt{0, 0, 0, 0, 0, 0};
     if (valid) {
         Stack st;
-        st.lds = lds_stack + tid;
+        st.lds = (lds_u64*)(lds_stack + tid);
         st.stride = blockDim.x;
         st.sp = 0;
         PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
@@ -567,6 +256,7 @@ struct DeviceReplica {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int64_t bytes = 0;
+    WaveBuffers wave;                         // wavefront-pipeline queues (grown on demand)
 };
 
 }  // namespace
@@ -589,6 +279,7 @@ static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
 
 static void free_replica(DeviceReplica& r) {
     (void)hipSetDevice(r.device);
+    wave_release(r.wave);
     (void)hipFree(r.recs); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
@@ -714,8 +405,26 @@ static bool scene_has_bounce(const HostScene& S) {
     return false;
 }
 
-static int32_t launch(const rt_scene* s, const DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {
+// MYRT_PATH=wave selects the wavefront pipeline (wavefront.hip); default: the
+// single-kernel path, currently the faster one on C3 (profiles/r01_*).
+static bool use_megakernel() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("MYRT_PATH");
+        v = (e && std::string(e) == "wave") ? 0 : 1;
+    }
+    return v == 1;
+}
+
+static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {
     if (P.num_chunks == 0) return RT_OK;
+    if (!use_megakernel()) {
+        const bool bounce_w = scene_has_bounce(s->host) && P.max_depth > 0;
+        const int32_t rc = wave_render(P, r.wave, bounce_w, count, stream);
+        if (rc != RT_OK) return fail(rc, rc == RT_ERR_OOM ? "device allocation of wavefront queues failed"
+                                                         : "wavefront launch failed");
+        return RT_OK;
+    }
     dim3 grid((unsigned)((P.cam.width + 31) / 32), (unsigned)P.num_chunks, 1);
     dim3 block(256, 1, 1);
     const size_t lds = (size_t)dev::kLds * 256 * sizeof(int2);
