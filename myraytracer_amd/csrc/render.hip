@@ -408,12 +408,8 @@ static bool scene_has_bounce(const HostScene& S) {
 // MYRT_PATH=wave selects the wavefront pipeline (wavefront.hip); default: the
 // single-kernel path, currently the faster one on C3 (profiles/r01_*).
 static bool use_megakernel() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("MYRT_PATH");
-        v = (e && std::string(e) == "wave") ? 0 : 1;
-    }
-    return v == 1;
+    const char* e = std::getenv("MYRT_PATH");   // read per launch so tests can A/B in one process
+    return !(e && std::strcmp(e, "wave") == 0);
 }
 
 static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {

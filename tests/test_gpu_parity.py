@@ -16,6 +16,13 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5   # per-channel L-inf, north_star
 
 
+@pytest.fixture(params=["mega", "wave"], autouse=True)
+def render_path(request, monkeypatch):
+    """Every parity test runs on both device pipelines (megakernel and wavefront)."""
+    monkeypatch.setenv("MYRT_PATH", request.param)
+    return request.param
+
+
 def _compare(sc, chunk_first=0, chunk_step=1, cam=0, tol=TOL, check_rgba=True):
     eng = M.RayTracerEngine(sc)
     rgb, rgba, st = eng.render_rows(cam, chunk_first, chunk_step, True)
