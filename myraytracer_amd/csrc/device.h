@@ -96,50 +96,89 @@ struct PCG32 {
 };
 
 // ----------------------------------------------------------------- traversal stack
-// Per-lane stack: the first kLds entries live in LDS ([slot][lane] so each lane hits
-// its own bank), deeper entries spill to a private array (scratch).  An entry is
-// {ref, entry distance rounded down to float} so far subtrees can be culled at pop.
+// Per-lane stack: the first kLds entries live in LDS ([slot][lane], so each lane hits its
+// own bank), deeper entries spill to a private (scratch) array that lives OUTSIDE the
+// struct: with a dynamically indexed array inside, the whole struct - `sp` included -
+// was demoted to scratch and every push stored `sp` to memory.
+// Pointers carry their address space explicitly: a plain pointer is generic and every
+// push/pop compiled to flat_* on the vector-memory path instead of ds_* / scratch_*.
+// An entry packs {ref (low 32), high 32 bits of the entry distance (high 32)}: dropping
+// the low mantissa word truncates toward zero, i.e. rounds a positive distance DOWN, so
+// pop-time culling stays conservative (negative distances are never culled).
 constexpr int kLds = 16;
 constexpr int kSpill = 64;
-// LDS-qualified pointer: a plain pointer is generic (flat) and every push/pop would
-// compile to flat_load/flat_store on the vector-memory path instead of ds_*.
-// An entry packs {ref (low 32 bits), entry distance as float bits (high 32 bits)}.
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+typedef __attribute__((address_space(5))) unsigned long long priv_u64;
 struct Stack {
     lds_u64* lds;        // &lds_base[threadIdx.x]; stride blockDim.x
+    priv_u64* spill;     // kSpill private entries
     int stride;
-    unsigned long long spill[kSpill];
     int sp;
-    // The empty asm in the rare spill branch keeps the compiler from merging the two
-    // accesses into one select-of-pointers (which would force a generic flat access).
-    __device__ __forceinline__ void push(int ref, float t) {
+    __device__ __forceinline__ void push(int ref, double t) {
         const unsigned long long e = (unsigned long long)(unsigned)ref |
-                                     ((unsigned long long)(unsigned)__float_as_int(t) << 32);
+                                     ((unsigned long long)(unsigned)__double2hiint(t) << 32);
         if (sp < kLds) {
             lds[sp * stride] = e;
         } else {
-            asm volatile("" ::: "memory");
+            asm volatile("" ::: "memory");   // keep the two stores apart (no select-of-pointers)
             spill[sp - kLds] = e;
         }
         ++sp;
     }
-    __device__ __forceinline__ int2 pop() {
+    // returns the ref; `tlo` = lower bound of the entry distance
+    __device__ __forceinline__ int pop(double& tlo) {
         --sp;
-        // unconditional ds_read of the clamped slot; the spill load only overrides it
-        unsigned long long e = lds[min(sp, kLds - 1) * stride];
+        unsigned long long e = lds[min(sp, kLds - 1) * stride];   // unconditional ds_read
         if (sp >= kLds) {
             asm volatile("" ::: "memory");
             e = spill[sp - kLds];
         }
-        return make_int2((int)(unsigned)(e & 0xffffffffull), (int)(unsigned)(e >> 32));
+        tlo = __hiloint2double((int)(unsigned)(e >> 32), 0);
+        return (int)(unsigned)(e & 0xffffffffull);
     }
 };
+#define MYRT_STACK(name, lds_base)                                   \
+    unsigned long long name##_spill_mem[kSpill];                     \
+    Stack name;                                                      \
+    name.lds = (lds_u64*)((lds_base) + threadIdx.x);                 \
+    name.spill = (priv_u64*)(name##_spill_mem);                      \
+    name.stride = blockDim.x;                                        \
+    name.sp = 0
 
 struct Counts { unsigned shadow, secondary; unsigned long long recs, tris, normals, insts; };
 
 struct Hit { double t, u, v; int tri, inst; };
 
-__device__ __forceinline__ float round_down_f(double d) { return __double2float_rd(d); }
+// Slab test with an explicit hit flag.  FAST = the ray has no zero direction component
+// (every 1/d finite), so no slab value can be NaN: then simd.min/max (minNum/maxNum)
+// and Swift.max/min agree on every comparison the caller makes (they can differ only in
+// the sign of a zero, which no comparison sees), and the scalar reductions become
+// v_max_f64 / v_min_f64 instead of compare+select pairs.  Otherwise the literal
+// NaN-asymmetric forms of hitAABB (RTContext.swift:557-565) are used.
+template <bool FAST>
+__device__ __forceinline__ bool slab_hit(double lx, double ly, double lz, double hx, double hy, double hz,
+                                         const V3& o, const V3& inv, double eps, double& tmin_out) {
+    const double t1x = (lx - o.x) * inv.x, t1y = (ly - o.y) * inv.y, t1z = (lz - o.z) * inv.z;
+    const double t2x = (hx - o.x) * inv.x, t2y = (hy - o.y) * inv.y, t2z = (hz - o.z) * inv.z;
+    const double mnx = fmin(t1x, t2x), mny = fmin(t1y, t2y), mnz = fmin(t1z, t2z);
+    const double mxx = fmax(t1x, t2x), mxy = fmax(t1y, t2y), mxz = fmax(t1z, t2z);
+    double tmin, tmax;
+    bool hit;
+    if (FAST) {
+        tmin = fmax(fmax(mnx, mny), mnz);
+        tmax = fmin(mxx, fmin(mxy, mxz));
+        hit = tmax >= fmax(tmin, eps);
+    } else {
+        tmin = smax(smax(mnx, mny), mnz);
+        tmax = smin(mxx, smin(mxy, mxz));
+        hit = tmax >= smax(tmin, eps);
+    }
+    tmin_out = tmin;
+    return hit;
+}
+__device__ __forceinline__ bool finite3(const V3& a) {
+    return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
+}
 
 // Closest-hit triangle test, intersectTriangle (RTContext.swift:479-510) minus the
 // hit-point/normal writes, which are recomputed once for the final hit (same values).
@@ -178,43 +217,66 @@ __device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, cons
     return (t > smax(eps, tlo) && t < thi);
 }
 
+// Test both children of inner record `ref`.  On return `ref` is the next node to visit
+// (true), or the caller must pop (false).  Order = near first, ties to L (the reference
+// pushes R then L after `if d1 > d2 swap`, RTContext.swift:600-606); the far child is
+// pushed.  Children beyond `lim` (conservative t-pruning) count as misses.
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
+                                           Stack& st, Counts& c) {
+    const WRec& R = P.recs[ref];
+    if (COUNT) c.recs++;
+    double t0, t1;
+    bool h0 = slab_hit<FAST>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv, P.eps, t0);
+    bool h1 = slab_hit<FAST>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv, P.eps, t1);
+    h0 = h0 && !(t0 > lim);
+    h1 = h1 && !(t1 > lim);
+    const int a = R.ref[0], b = R.ref[1];
+    if (h0 && h1) {
+        const bool sw = t0 > t1;
+        st.push(sw ? a : b, sw ? t0 : t1);
+        ref = sw ? b : a;
+        return true;
+    }
+    if (h0) { ref = a; return true; }
+    if (h1) { ref = b; return true; }
+    return false;
+}
+
+// Pop the next node whose entry distance does not exceed `lim`; false when the stack
+// (down to `base`) is exhausted.
+__device__ __forceinline__ bool pop_next(Stack& st, int base, double lim, int& ref) {
+    while (st.sp > base) {
+        double tlo;
+        const int r = st.pop(tlo);
+        if (tlo > lim) continue;
+        ref = r;
+        return true;
+    }
+    return false;
+}
+
 // One ordered BVH walk shared by the closest-hit and any-hit queries.  `ref` is a
 // node the caller has already tested (the root); children are tested at the parent
-// (one 128-B record holds both), near pushed last (RTContext.swift:600-606).
-// LEAF(ref) handles a leaf run and returns true to terminate the walk (any-hit).
-// LIMIT() gives the current pruning distance.
-template <bool COUNT, class Leaf, class Limit>
+// (one 128-B record holds both).  LEAF(ref) handles a leaf run and returns true to
+// terminate the walk (any-hit).  LIMIT() gives the current pruning distance.
+template <bool COUNT, bool FAST, class Leaf, class Limit>
 __device__ __forceinline__ bool walk(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st, int base,
                                      Counts& c, Leaf leaf, Limit limit) {
-    const double eps = P.eps;
     for (;;) {
         if (ref >= 0) {
-            const WRec& R = P.recs[ref];
-            if (COUNT) c.recs++;
-            double d0 = slab(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv, eps);
-            double d1 = slab(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv, eps);
-            const double lim = limit();
-            if (d0 > lim) d0 = DINF;
-            if (d1 > lim) d1 = DINF;
-            int a = R.ref[0], b = R.ref[1];
-            if (d0 > d1) { const double td = d0; d0 = d1; d1 = td; const int tr = a; a = b; b = tr; }
-            if (d0 != DINF) {
-                if (d1 != DINF) st.push(b, round_down_f(d1));
-                ref = a;
-                continue;
-            }
+            if (inner_step<COUNT, FAST>(P, ref, o, inv, limit(), st, c)) continue;
         } else {
             if (leaf(ref)) return true;
         }
-        // pop, culling entries that start beyond the current limit
-        for (;;) {
-            if (st.sp == base) return false;
-            const int2 e = st.pop();
-            if ((double)__int_as_float(e.y) > limit()) continue;
-            ref = e.x;
-            break;
-        }
+        if (!pop_next(st, base, limit(), ref)) return false;
     }
+}
+template <bool COUNT, class Leaf, class Limit>
+__device__ __forceinline__ bool walk_any(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st,
+                                         int base, Counts& c, Leaf leaf, Limit limit) {
+    if (__all(finite3(inv))) return walk<COUNT, true>(P, ref, o, inv, st, base, c, leaf, limit);
+    return walk<COUNT, false>(P, ref, o, inv, st, base, c, leaf, limit);
 }
 
 template <bool COUNT>
@@ -223,11 +285,12 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
     const double eps = P.eps;
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     auto limit = [&]() { return h.t * P.prune_rel + P.prune_abs; };   // prune_rel = 1 + delta
-    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
-                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
-    if (d0 == DINF) return;
+    double d0;
+    if (!slab_hit<false>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
+                         P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps, d0))
+        return;
     auto tlas_leaf = [&](int ref) -> bool {
-        for (int e = ~ref;; ++e) {
+        for (int e = ~ref - P.tlas_leaf_base;; ++e) {
             const DTlasLeafEntry le = P.tlas_leaf[e];
             const DInstance& I = P.insts[le.inst];
             if (COUNT) c.insts++;
@@ -237,9 +300,9 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
             const V3 ol = m4_point(I.w2l, ow, 1.0);
             const V3 dl = m4_point(I.w2l, d, 0.0);
             const V3 il = rcp(dl);
-            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
-                                   I.root_hi[2], ol, il, eps);
-            if (dr != DINF && !(dr > limit())) {
+            double dr;
+            if (slab_hit<false>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1], I.root_hi[2],
+                                ol, il, eps, dr) && !(dr > limit())) {
                 const V3 omb = ol - ld3(I.tri_motion) * time;   // Triangle.motionBlur offset (:480-481)
                 const int inst = le.inst;
                 auto blas_leaf = [&](int r) -> bool {
@@ -253,7 +316,7 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
                 };
                 const int sbase = st.sp;
                 if (I.root_ref < 0) blas_leaf(I.root_ref);
-                else walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+                else walk_any<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
             }
             if (le.last) break;
         }
@@ -261,7 +324,7 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
     };
     const int base = st.sp;
     if (P.tlas_root_ref < 0) tlas_leaf(P.tlas_root_ref);
-    else walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+    else walk_any<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
 }
 
 template <bool COUNT>
@@ -272,11 +335,12 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
     const V3 inv = rcp(d);
     const double lim = tmax * P.prune_rel + P.prune_abs;
     auto limit = [&]() { return lim; };
-    const double d0 = slab(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
-                           P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps);
-    if (d0 == DINF || d0 > lim) return false;
+    double d0;
+    if (!slab_hit<false>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
+                         P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps, d0) || d0 > lim)
+        return false;
     auto tlas_leaf = [&](int ref) -> bool {
-        for (int e = ~ref;; ++e) {
+        for (int e = ~ref - P.tlas_leaf_base;; ++e) {
             const DTlasLeafEntry le = P.tlas_leaf[e];
             const DInstance& I = P.insts[le.inst];
             if (COUNT) c.insts++;
@@ -284,9 +348,9 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
             const V3 ol = m4_point(I.w2l, o - instOffset, 1.0);
             const V3 dl = m4_point(I.w2l, d, 0.0);
             const V3 il = rcp(dl);
-            const double dr = slab(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
-                                   I.root_hi[2], ol, il, eps);
-            if (dr != DINF && !(dr > lim)) {
+            double dr;
+            if (slab_hit<false>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1], I.root_hi[2],
+                                ol, il, eps, dr) && !(dr > lim)) {
                 const V3 omb = ol - ld3(I.tri_motion) * time;
                 auto blas_leaf = [&](int r) -> bool {
                     for (int t = ~r;; ++t) {
@@ -300,7 +364,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
                 const int sbase = st.sp;
                 bool hit;
                 if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
-                else hit = walk<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+                else hit = walk_any<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
                 if (hit) { st.sp = sbase; return true; }
             }
             if (le.last) break;
@@ -310,9 +374,66 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
     const int base = st.sp;
     bool hit;
     if (P.tlas_root_ref < 0) hit = tlas_leaf(P.tlas_root_ref);
-    else hit = walk<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+    else hit = walk_any<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
     st.sp = base;
     return hit;
+}
+
+// ---------------------------------------------------------- unified identity walk
+// When every instance is the identity and static (HostScene::identity), the local ray
+// equals the world ray, so TLAS and BLAS records are walked as ONE tree with one stack:
+// a TLAS leaf pushes its instances' BLAS roots (tested with the world ray) in reverse
+// order, so they pop - and are traversed fully - in leaf order, as intersectTLAS does
+// (RTContext.swift:648-706).  One call = one step: one inner record or one leaf run,
+// followed by the pop of the next node.  Returns 0 = continue, 1 = stack exhausted,
+// 2 = shadow ray occluded.
+template <bool COUNT, bool SHADOW, bool FAST>
+__device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Stack& st, const V3& o, const V3& d,
+                                            const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
+    const double eps = P.eps;
+    if (ref >= 0) {
+        if (inner_step<COUNT, FAST>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c))
+            return 0;
+    } else {
+        const int e = ~ref;
+        if (e < P.tlas_leaf_base) {                                  // BLAS leaf run
+            for (int t = e;; ++t) {
+                const TriRec& T = P.tris[t];
+                if (COUNT) c.tris++;
+                if (SHADOW) {
+                    if (tri_shadow(T, o, d, 0.0, tmax, eps)) return 2;
+                } else {
+                    tri_closest(T, o, d, tlo, eps, h, t, T.prim);     // prim = owning instance
+                }
+                if (T.last) break;
+            }
+        } else {                                                      // TLAS leaf: instance list
+            const int k0 = e - P.tlas_leaf_base;
+            int k1 = k0;
+            while (!P.tlas_leaf[k1].last) ++k1;
+            const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+            for (int k = k1; k >= k0; --k) {
+                const DInstance& I = P.insts[P.tlas_leaf[k].inst];
+                if (COUNT) c.insts++;
+                double dr;
+                if (slab_hit<FAST>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                                   I.root_hi[2], o, inv, eps, dr) && !(dr > lim))
+                    st.push(I.root_ref, dr);
+            }
+        }
+    }
+    return pop_next(st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref) ? 0 : 1;
+}
+
+// Root test of the unified walk (the TLAS root is popped and tested first,
+// RTContext.swift:642-646).  Returns false when the ray misses the whole scene.
+__device__ __forceinline__ bool unified_begin(const RenderParams& P, const V3& o, const V3& inv, double lim, int& ref) {
+    double d0;
+    if (!slab_hit<false>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
+                         P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, P.eps, d0) || d0 > lim)
+        return false;
+    ref = P.tlas_root_ref;
+    return true;
 }
 
 // orthonormalBasis (Object+Extension.swift:531-552)

@@ -19,9 +19,9 @@ namespace myrt {
 
 // Child reference encoding used in WRec.ref[], stack entries and instance roots:
 //   ref >= 0 : inner node -> index of its WRec
-//   ref <  0 : leaf       -> ~ref = index of its first TriRec (BLAS) or first
-//                            TLAS leaf-list entry; the run ends at the entry whose
-//                            `last` flag is set.
+//   ref <  0 : leaf       -> ~ref = index of its first TriRec (BLAS leaf), or
+//                            tlas_leaf_base + index of its first TLAS leaf-list entry;
+//                            the run ends at the entry whose `last` flag is set.
 struct alignas(128) WRec {
     double lo[2][3];      // child c aabbMin (x,y,z)
     double hi[2][3];      // child c aabbMax
@@ -33,7 +33,7 @@ static_assert(sizeof(WRec) == 128, "WRec must be one 128-B line");
 struct alignas(16) TriRec {
     double v0[3], e1[3], e2[3];
     int32_t last;         // 1 = last triangle of its leaf
-    int32_t prim;         // original triangle index (reference `triangles[]` order)
+    int32_t prim;         // identity mode: owning instance; otherwise the reference `triangles[]` index
 };
 static_assert(sizeof(TriRec) == 80, "TriRec is 80 B");
 
@@ -80,6 +80,8 @@ struct RenderParams {
     double tlas_root_lo[3], tlas_root_hi[3];
     int32_t tlas_root_ref;
     int32_t has_tlas;
+    int32_t tlas_leaf_base;          // TriRec count: ~ref >= base means a TLAS leaf
+    int32_t identity;                // unified TLAS+BLAS walk allowed (scene.h HostScene::identity)
     int32_t num_mats;
     int32_t num_plights;
     DCamera cam;

@@ -149,10 +149,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     const bool valid = (i < C.width) && (j < C.height);
     Counts cnt{0, 0, 0, 0, 0, 0};
     if (valid) {
-        Stack st;
-        st.lds = (lds_u64*)(lds_stack + tid);
-        st.stride = blockDim.x;
-        st.sp = 0;
+        MYRT_STACK(st, lds_stack);
         PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
         V3 pixel = v3(0, 0, 0);
         const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
@@ -382,6 +379,8 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     for (int k = 0; k < 3; ++k) { P.tlas_root_lo[k] = S.tlas_root_lo[k]; P.tlas_root_hi[k] = S.tlas_root_hi[k]; }
     P.tlas_root_ref = S.tlas_root_ref;
     P.has_tlas = S.has_tlas ? 1 : 0;
+    P.tlas_leaf_base = (int32_t)S.tlas_leaf_base;
+    P.identity = S.identity ? 1 : 0;
     P.num_mats = (int32_t)S.mats.size();
     P.num_plights = (int32_t)S.plights.size();
     P.cam = camera_constants(S.cams[cam]);

@@ -281,6 +281,7 @@ struct BlasBuild {
     int64_t depth = 0;
     // filled by layout
     int32_t root_ref = 0;
+    int64_t tri_first = 0, tri_end = 0;   // run of this BLAS's TriRecs in HostScene::tris
     double root_lo[3], root_hi[3];
 };
 struct InstBuild { int blas; double M[16]; int material; D3 motion; double wlo[3], whi[3]; };
@@ -551,7 +552,9 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             }
             return first;
         };
+        bb.tri_first = (int64_t)S.tris.size();
         bb.root_ref = layout_bvh(bb.bvh, S.recs, emit);
+        bb.tri_end = (int64_t)S.tris.size();
         for (int k = 0; k < 3; ++k) { bb.root_lo[k] = bb.bvh.lo[k]; bb.root_hi[k] = bb.bvh.hi[k]; }
         bb.bvh = RefBVH();   // free host copy
         bb.prims = PrimSet();
@@ -609,8 +612,10 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         S.tlas_hash = ref_bvh_hash(tb, ident);
         const int64_t tdepth = ref_bvh_depth(tb);
         for (int k = 0; k < 3; ++k) { S.tlas_root_lo[k] = tb.lo[k]; S.tlas_root_hi[k] = tb.hi[k]; }
+        // TLAS leaf refs are offset by the TriRec count so one ref space covers both levels
+        S.tlas_leaf_base = (int64_t)S.tris.size();
         auto emit = [&](int64_t firstSlot, int64_t count) -> int64_t {
-            const int64_t first = (int64_t)S.tlas_leaf.size();
+            const int64_t first = S.tlas_leaf_base + (int64_t)S.tlas_leaf.size();
             for (int64_t q = 0; q < count; ++q)
                 S.tlas_leaf.push_back(DTlasLeafEntry{(int32_t)tb.primIdx[firstSlot + q], (q == count - 1) ? 1 : 0});
             return first;
@@ -622,6 +627,30 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         const double dx = whi[0] - wlo[0], dy = whi[1] - wlo[1], dz = whi[2] - wlo[2];
         S.scene_extent = std::sqrt(dx * dx + dy * dy + dz * dz);
         if (!std::isfinite(S.scene_extent) || S.scene_extent <= 0) S.scene_extent = 1.0;
+    }
+    // Identity mode: every instance's transforms are exactly the identity and nothing moves,
+    // so the world ray IS the local ray (up to the sign of zeros, which no comparison sees)
+    // and TLAS + BLAS records can be walked as one tree with one stack.  Each BLAS must
+    // belong to exactly one instance so a triangle identifies its instance.
+    {
+        bool ident = S.has_tlas;
+        std::vector<int> owners(blases.size(), 0);
+        for (size_t i = 0; i < insts.size() && ident; ++i) {
+            const InstBuild& ib = insts[i];
+            for (int k = 0; k < 16; ++k) ident &= ib.M[k] == ((k % 5 == 0) ? 1.0 : 0.0);
+            ident &= ib.motion.x == 0 && ib.motion.y == 0 && ib.motion.z == 0;
+            const BlasBuild& bb = blases[ib.blas];
+            ident &= bb.motion.x == 0 && bb.motion.y == 0 && bb.motion.z == 0;
+            owners[ib.blas]++;
+        }
+        for (int o : owners) ident &= (o <= 1);
+        S.identity = ident;
+        if (ident) {
+            for (size_t i = 0; i < insts.size(); ++i) {
+                const BlasBuild& bb = blases[insts[i].blas];
+                for (int64_t t = bb.tri_first; t < bb.tri_end; ++t) S.tris[t].prim = (int32_t)i;
+            }
+        }
     }
     if (S.recs.size() >= (size_t)INT32_MAX || S.tris.size() >= (size_t)INT32_MAX) { err = "scene too large for int32 refs"; return RT_ERR_UNSUPPORTED; }
     if (maxBlasDepth + 1 > 63) { err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550)"; return RT_ERR_STACK; }

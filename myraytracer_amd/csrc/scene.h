@@ -56,7 +56,9 @@ struct HostScene {
     std::vector<DTlasLeafEntry> tlas_leaf;
     double tlas_root_lo[3] = {0, 0, 0}, tlas_root_hi[3] = {0, 0, 0};
     int32_t tlas_root_ref = 0;
+    int64_t tlas_leaf_base = 0;            // TLAS leaf refs are ~(tlas_leaf_base + entry)
     bool has_tlas = false;
+    bool identity = false;                 // all instances identity & static (unified walk)
     int64_t blas_records = 0, tlas_records = 0;
     int64_t max_stack = 0;                 // LDS stack entries a traversal needs
     double scene_extent = 1.0;             // world bounds diagonal (pruning margin scale)

@@ -24,7 +24,7 @@ struct WaveBuffers {
     int32_t* term = nullptr;               // [P] terminal level (| kMissFlag)
     unsigned long long* rng = nullptr;     // [P][2] PCG32 state, inc
     double* accum = nullptr;               // [P][3] sample sum
-    unsigned* qcount = nullptr;            // [64] queue counters (zeroed per frame)
+    unsigned* qcount = nullptr;            // 8 XCD-homed work counters per traversal launch
     int64_t bytes = 0;
 };
 

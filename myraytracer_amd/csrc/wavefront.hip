@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/rtcore.h"
@@ -35,8 +36,7 @@ struct ShadowContrib { double c[3]; int32_t has, pad; };                        
 struct ShadeOut { double lo[3]; int32_t first, n; };                                           // 32 B
 
 constexpr int32_t kMissFlag = 1 << 30;
-constexpr int kQTrace = 0;    // qcount[kQTrace + d]  : trace queue length at level d (d >= 1)
-constexpr int kQShadow = 24;  // qcount[kQShadow + d] : shadow queue length at level d
+constexpr int kCounterSlots = 4096;   // traversal launches per frame (8 work counters each)
 
 struct WaveParams {
     RenderParams R;
@@ -60,22 +60,6 @@ struct WaveParams {
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-
-// Exclusive prefix of `n` over the wave + one atomic reservation in `counter`.
-__device__ __forceinline__ unsigned wave_append(unsigned* counter, unsigned n) {
-    const int lane = lane_id();
-    unsigned incl = n;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const unsigned y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    const unsigned total = __shfl(incl, 63, 64);
-    unsigned base = 0;
-    if (lane == 0 && total) base = atomicAdd(counter, total);
-    base = __shfl(base, 0, 64);
-    return base + incl - n;
-}
 
 struct PixelOf { int i, j, outRow; bool valid; };
 __device__ __forceinline__ PixelOf pixel_of(const WaveParams& W, int64_t slot) {
@@ -103,128 +87,265 @@ __device__ __forceinline__ void flush_counts(const WaveParams& W, const Counts& 
     }
 }
 
-// ---------------------------------------------------------------------- k_trace
-// Level 0: generate the primary ray of (pixel, sample) exactly as Renderer.render does
-// (Object+Extension.swift:294-344) and trace it; level >= 1: trace the bounce queue.
-template <bool COUNT, bool PRIMARY>
-__global__ __launch_bounds__(256) void k_trace(WaveParams W) {
+// Queues are indexed by PATH (= primary pixel slot) at every level, not compacted: an
+// empty entry is marked (TraceItem.path < 0, ShadowItem.tmax < 0).  Compaction by
+// per-wave atomics on one counter serialises (~88 adds/us for one word,
+// MI355X_MICROARCH "dequeue"); the persistent traversal kernels below skip empty
+// entries at fetch time instead, so no short kernel issues same-address atomics.
+
+// ------------------------------------------------------------------ ray generation
+// Primary ray of (pixel, sample) exactly as Renderer.render (Object+Extension.swift:294-344).
+__device__ __forceinline__ void gen_primary(const WaveParams& W, const PixelOf& px, int64_t slot, V3& o, V3& d,
+                                            double& tlo, double& time) {
+    const DCamera& C = W.R.cam;
+    unsigned long long* rs = W.rng + 2 * slot;
+    PCG32 rng(0ull);
+    if (W.sample == 0) {
+        rng = PCG32((((unsigned long long)px.j << 32) ^ (unsigned long long)px.i) + 0x9E3779B97F4A7C15ull);
+    } else {
+        rng.state = rs[0];
+        rng.inc = rs[1];
+    }
+    const int sx = W.sample % C.n, sy = W.sample / C.n;
+    const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
+    const double xi1 = rng.nextFloat();
+    const double xi2 = rng.nextFloat();
+    const double iOffset = ((double)sx + xi1) / (double)C.n;
+    const double jOffset = ((double)sy + xi2) / (double)C.n;
+    const double currentI = (double)px.i + iOffset;
+    const double currentJ = (double)px.j + jOffset;
+    const V3 s = (q00 - v * (currentJ * C.dv)) + u * (currentI * C.du);
+    const V3 dir0 = normalize(s - eye);
+    V3 dir = dir0, camEye = eye;
+    if (C.aperture > 0 && C.focus > 0) {                       // DOF (:325-338)
+        const double denom = dot(dir0, -w);
+        const double tFocus = fabs(denom) < 1e-6 ? C.focus : (C.focus / denom);
+        const V3 pFocus = eye + dir0 * tFocus;
+        const double uRand = rng.nextFloat() - 0.5;
+        const double vRand = rng.nextFloat() - 0.5;
+        const V3 a = eye + ((uRand * u) + (vRand * v)) * C.aperture;
+        dir = normalize(pFocus - a);
+        camEye = a;
+    }
+    time = rng.nextFloat();
+    const double denom = dot(dir, w);
+    const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
+    tlo = smax(tImg, 0.0);
+    rs[0] = rng.state;
+    rs[1] = rng.inc;
+    o = camEye;
+    d = dir;
+    TraceItem it;
+    it.o[0] = o.x; it.o[1] = o.y; it.o[2] = o.z;
+    it.d[0] = d.x; it.d[1] = d.y; it.d[2] = d.z;
+    it.tlo = tlo; it.time = time; it.path = (int32_t)slot; it.pad = 0;
+    W.items[0][slot] = it;
+}
+
+// Fetch item `slot` of the current level: returns false for an empty entry.
+template <int MODE>   // 0 = primary, 1 = bounce queue, 2 = shadow queue
+__device__ __forceinline__ bool fetch_item(const WaveParams& W, int64_t slot, V3& o, V3& d, double& tlo,
+                                           double& tmax, double& time) {
+    if (MODE == 0) {
+        const PixelOf px = pixel_of(W, slot);
+        if (!px.valid) return false;
+        gen_primary(W, px, slot, o, d, tlo, time);
+        tmax = DINF;
+        return true;
+    } else if (MODE == 1) {
+        const TraceItem& it = W.items[W.depth & 1][slot];
+        if (it.path < 0) return false;
+        o = ld3(it.o); d = ld3(it.d); tlo = it.tlo; time = it.time; tmax = DINF;
+        return true;
+    } else {
+        const ShadowItem& si = W.shadows[slot];
+        if (!(si.tmax >= 0.0)) return false;
+        o = ld3(si.o); d = ld3(si.d); tmax = si.tmax; time = si.time; tlo = 0.0;
+        return true;
+    }
+}
+
+// ------------------------------------------------------- persistent traversal (identity)
+// Every wave keeps 64 rays in flight and refills lanes whose ray finished from a
+// work pool (Aila & Laine's persistent threads with ray replacement): lane utilisation
+// no longer decays with the longest ray of a tile.  Work is split into 8 home ranges,
+// one per XCD (blocks are dealt round-robin to XCDs, so block b runs on XCD b % 8):
+// a wave grabs 64-item tiles from its home range - neighbouring image tiles share an
+// L2 - and steals from the other ranges once its own is exhausted.
+constexpr int kGrab = 64;
+constexpr int kRefillMin = 16;
+
+struct WaveWork {
+    int64_t next, end;
+    int home, tries;
+    bool done;
+};
+
+__device__ __forceinline__ bool grab_work(WaveWork& w, unsigned* ctr, int64_t N) {
+    const int64_t R = ((N + 7) / 8 + kGrab - 1) / kGrab * kGrab;
+    while (w.tries < 8) {
+        const int h = (w.home + w.tries) & 7;
+        const int64_t base = (int64_t)h * R, lim = min(N, base + R);
+        unsigned got = 0;
+        if (lane_id() == 0 && base < lim) got = atomicAdd(&ctr[h], (unsigned)kGrab);
+        got = __shfl(got, 0, 64);
+        if (base + (int64_t)got < lim) {
+            w.next = base + got;
+            w.end = min(lim, w.next + kGrab);
+            return true;
+        }
+        w.tries++;
+    }
+    w.done = true;
+    return false;
+}
+
+template <bool COUNT, int MODE>
+__global__ __launch_bounds__(256) void k_persist(WaveParams W, int64_t N, unsigned* ctr) {
+    extern __shared__ unsigned long long lds_stack[];
+    const RenderParams& P = W.R;
+    constexpr bool SHADOW = (MODE == 2);
+    MYRT_STACK(st, lds_stack);
+    Counts cnt{0, 0, 0, 0, 0, 0};
+    const int lane = lane_id();
+    const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    WaveWork w{0, 0, (int)(blockIdx.x & 7), 0, false};
+    int64_t slot = -1;
+    int ref = 0;
+    V3 o{0, 0, 0}, d{0, 0, 0}, inv{0, 0, 0};
+    double tlo = 0, tmax = DINF, time = 0;
+    Hit h;
+    h.t = DINF; h.u = 0; h.v = 0; h.tri = -1; h.inst = -1;
+    unsigned rays = 0;
+    for (;;) {
+        // ---- refill idle lanes (wave-uniform decision)
+        const unsigned long long idle = __ballot(slot < 0);
+        const int nIdle = __popcll(idle);
+        if (!w.done && (nIdle >= kRefillMin || nIdle == 64)) {
+            const int rank = __popcll(idle & ltMask);
+            int assigned = 0;
+            int64_t mine = -1;
+            while (assigned < nIdle) {
+                if (w.next >= w.end && !grab_work(w, ctr, N)) break;
+                const int take = (int)min((int64_t)(nIdle - assigned), w.end - w.next);
+                if (slot < 0 && rank >= assigned && rank < assigned + take) mine = w.next + (rank - assigned);
+                w.next += take;
+                assigned += take;
+            }
+            if (mine >= 0) {
+                slot = mine;
+                bool live = fetch_item<MODE>(W, slot, o, d, tlo, tmax, time);
+                if (live) {
+                    rays++;
+                    inv = rcp(d);
+                    h.t = DINF; h.u = 0; h.v = 0; h.tri = -1; h.inst = -1;
+                    st.sp = 0;
+                    live = unified_begin(P, o, inv, SHADOW ? tmax * P.prune_rel + P.prune_abs : DINF, ref);
+                    if (!live) {                                   // missed the whole scene
+                        if (SHADOW) W.occluded[slot] = 0;
+                        else {
+                            HitOut ho; ho.t = DINF; ho.u = 0; ho.v = 0; ho.tri = -1; ho.inst = -1;
+                            W.hits[slot] = ho;
+                        }
+                    }
+                }
+                if (!live) slot = -1;
+            }
+        }
+        if (__ballot(slot >= 0) == 0) {
+            if (w.done) break;
+            continue;
+        }
+        // ---- one traversal step per live lane (FAST slabs unless some live ray has a
+        //      zero direction component, see slab_hit)
+        const bool fast = __all(slot < 0 || finite3(inv));
+        if (slot >= 0) {
+            const int r = fast ? unified_step<COUNT, SHADOW, true>(P, ref, st, o, d, inv, tlo, tmax, h, cnt)
+                               : unified_step<COUNT, SHADOW, false>(P, ref, st, o, d, inv, tlo, tmax, h, cnt);
+            if (r != 0) {
+                if (SHADOW) {
+                    W.occluded[slot] = (r == 2) ? 1 : 0;
+                } else {
+                    HitOut ho; ho.t = h.t; ho.u = h.u; ho.v = h.v; ho.tri = h.tri; ho.inst = h.inst;
+                    W.hits[slot] = ho;
+                }
+                slot = -1;
+            }
+        }
+    }
+    // ray counters: shadow rays (MODE 2) and secondary rays (MODE 1), one atomic per wave
+    const unsigned long long nr = wave_sum((unsigned long long)rays);
+    if (lane == 0 && nr) {
+        if (MODE == 2) atomicAdd(&P.counters[0], nr);
+        if (MODE == 1) atomicAdd(&P.counters[1], nr);
+    }
+    flush_counts(W, cnt, COUNT);
+}
+
+// ------------------------------------------------------- general traversal (any instances)
+template <bool COUNT, int MODE>
+__global__ __launch_bounds__(256) void k_general(WaveParams W, int64_t N) {
     extern __shared__ unsigned long long lds_stack[];
     const RenderParams& P = W.R;
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     Counts cnt{0, 0, 0, 0, 0, 0};
-    bool active;
+    unsigned rays = 0;
     V3 o, d;
-    double tlo, time;
-    if (PRIMARY) {
-        active = slot < W.P;
-        PixelOf px = active ? pixel_of(W, slot) : PixelOf{0, 0, 0, false};
-        if (active && !px.valid) {
-            W.items[0][slot].path = -1;
-            active = false;
-        }
-        if (active) {
-            const DCamera& C = P.cam;
-            unsigned long long* rs = W.rng + 2 * slot;
-            PCG32 rng(0ull);
-            if (W.sample == 0) {
-                rng = PCG32((((unsigned long long)px.j << 32) ^ (unsigned long long)px.i) + 0x9E3779B97F4A7C15ull);
-            } else {
-                rng.state = rs[0];
-                rng.inc = rs[1];
-            }
-            const int sx = W.sample % C.n, sy = W.sample / C.n;
-            const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
-            const double xi1 = rng.nextFloat();
-            const double xi2 = rng.nextFloat();
-            const double iOffset = ((double)sx + xi1) / (double)C.n;
-            const double jOffset = ((double)sy + xi2) / (double)C.n;
-            const double currentI = (double)px.i + iOffset;
-            const double currentJ = (double)px.j + jOffset;
-            const V3 s = (q00 - v * (currentJ * C.dv)) + u * (currentI * C.du);
-            const V3 dir0 = normalize(s - eye);
-            V3 dir = dir0, camEye = eye;
-            if (C.aperture > 0 && C.focus > 0) {                       // DOF (:325-338)
-                const double denom = dot(dir0, -w);
-                const double tFocus = fabs(denom) < 1e-6 ? C.focus : (C.focus / denom);
-                const V3 pFocus = eye + dir0 * tFocus;
-                const double uRand = rng.nextFloat() - 0.5;
-                const double vRand = rng.nextFloat() - 0.5;
-                const V3 a = eye + ((uRand * u) + (vRand * v)) * C.aperture;
-                dir = normalize(pFocus - a);
-                camEye = a;
-            }
-            time = rng.nextFloat();
-            const double denom = dot(dir, w);
-            const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
-            tlo = smax(tImg, 0.0);
-            rs[0] = rng.state;
-            rs[1] = rng.inc;
-            o = camEye;
-            d = dir;
-            TraceItem it;
-            it.o[0] = o.x; it.o[1] = o.y; it.o[2] = o.z;
-            it.d[0] = d.x; it.d[1] = d.y; it.d[2] = d.z;
-            it.tlo = tlo; it.time = time; it.path = (int32_t)slot; it.pad = 0;
-            W.items[0][slot] = it;
-        }
-    } else {
-        active = slot < (int64_t)W.qcount[kQTrace + W.depth];
-        if (active) {
-            const TraceItem& it = W.items[W.depth & 1][slot];
-            o = ld3(it.o); d = ld3(it.d); tlo = it.tlo; time = it.time;
+    double tlo, tmax, time;
+    if (slot < N && fetch_item<MODE>(W, slot, o, d, tlo, tmax, time)) {
+        rays = 1;
+        MYRT_STACK(st, lds_stack);
+        if (MODE == 2) {
+            W.occluded[slot] = occluded<COUNT>(P, o, d, tmax, time, st, cnt) ? 1 : 0;
+        } else {
+            Hit h;
+            if (P.has_tlas) intersect_closest<COUNT>(P, o, d, rcp(d), tlo, time, h, st, cnt);
+            else { h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0; }
+            HitOut ho; ho.t = h.t; ho.u = h.u; ho.v = h.v; ho.tri = h.tri; ho.inst = h.inst;
+            W.hits[slot] = ho;
         }
     }
-    if (active) {
-        Stack st;
-        st.lds = (lds_u64*)(lds_stack + threadIdx.x);
-        st.stride = blockDim.x;
-        st.sp = 0;
-        Hit h;
-        if (P.has_tlas) {
-            intersect_closest<COUNT>(P, o, d, rcp(d), tlo, time, h, st, cnt);
-        } else {
-            h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-        }
-        HitOut ho;
-        ho.t = h.t; ho.u = h.u; ho.v = h.v; ho.tri = h.tri; ho.inst = h.inst;
-        W.hits[slot] = ho;
+    const unsigned long long nr = wave_sum((unsigned long long)rays);
+    if (lane_id() == 0 && nr) {
+        if (MODE == 2) atomicAdd(&P.counters[0], nr);
+        if (MODE == 1) atomicAdd(&P.counters[1], nr);
     }
     flush_counts(W, cnt, COUNT);
 }
 
 // ---------------------------------------------------------------------- k_shade
+// One lane per path: hit reconstruction, material, direct-light terms, shadow rays
+// (path*L + l) and the bounce ray (same path slot, next level).
 template <bool COUNT, bool BOUNCE>
 __global__ __launch_bounds__(256) void k_shade(WaveParams W) {
     const RenderParams& P = W.R;
     const int depth = W.depth;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t count = depth == 0 ? W.P : (int64_t)W.qcount[kQTrace + depth];
+    const int64_t path = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (path >= W.P) return;
     Counts cnt{0, 0, 0, 0, 0, 0};
-    bool active = slot < count;
-    TraceItem it;
-    HitOut h;
-    int32_t path = -1;
-    if (active) {
-        it = W.items[depth & 1][slot];
-        path = it.path;
-        active = path >= 0;
-    }
-    if (active) h = W.hits[slot];
     const int L = P.num_plights;
-    bool hit = active && h.inst >= 0 && P.has_tlas;
-    unsigned nShadow = 0;
+    bool active;
+    TraceItem it;
+    if (depth == 0) {
+        active = pixel_of(W, path).valid;
+        if (active) it = W.items[0][path];
+    } else {
+        it = W.items[depth & 1][path];
+        active = it.path >= 0;
+    }
+    HitOut h;
+    if (active) h = W.hits[path];
+    const bool hit = active && h.inst >= 0 && P.has_tlas;
     bool bounce = false;
-    V3 p{0, 0, 0}, N{0, 0, 0}, Lo{0, 0, 0}, rd{0, 0, 0}, mult{0, 0, 0};
-    V3 d{0, 0, 0};
-    const DMaterial* Mp = nullptr;
     if (active && !hit) {                         // miss -> backgroundColor (:101-103); no TLAS -> 0 (:98)
         W.term[path] = depth | kMissFlag;
         double* lo = W.lod + ((size_t)depth * W.P + path) * 3;
         if (P.has_tlas) { lo[0] = P.background[0]; lo[1] = P.background[1]; lo[2] = P.background[2]; }
         else { lo[0] = 0.0; lo[1] = 0.0; lo[2] = 0.0; }
     }
+    unsigned nShadow = 0;
     if (hit) {
-        d = ld3(it.d);
+        const V3 d = ld3(it.d);
         const double time = it.time;
         const TriRec& T = P.tris[h.tri];
         const DInstance& I = P.insts[h.inst];
@@ -239,27 +360,62 @@ __global__ __launch_bounds__(256) void k_shade(WaveParams W) {
             nl = normalize(cross(e1, e2));
         }
         const V3 pl = (v0 + (h.u * e1)) + (h.v * e2);
-        p = m4_point(I.l2w, pl, 1.0) + ld3(I.motion) * time;
+        const V3 p = m4_point(I.l2w, pl, 1.0) + ld3(I.motion) * time;
         V3 Ngeo = normalize(m3_mul(I.nmat, nl));
         if (I.det_neg) Ngeo = -Ngeo;
         const int matIndex = max(0, min(P.num_mats - 1, I.material - 1));
-        Mp = &P.mats[matIndex];
-        const DMaterial& M = *Mp;
+        const DMaterial& M = P.mats[matIndex];
         const bool frontFacing = dot(d, Ngeo) < 0;
-        N = frontFacing ? Ngeo : -Ngeo;
+        const V3 N = frontFacing ? Ngeo : -Ngeo;
         const bool computeDirect = !(M.ior > 0) || frontFacing;
-        Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+        const V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
         nShadow = computeDirect ? (unsigned)L : 0u;
+        ShadeOut so;
+        so.lo[0] = Lo.x; so.lo[1] = Lo.y; so.lo[2] = Lo.z;
+        so.first = (int32_t)(path * L);
+        so.n = (int32_t)nShadow;
+        W.shade[path] = so;
+        for (int li = 0; li < (int)nShadow; ++li) {                 // :118-143
+            const DPointLight& PL = P.plights[li];
+            V3 wi = ld3(PL.position) - p;
+            const double dist = length(wi);
+            wi = normalize(wi);
+            const V3 so3 = p + wi * P.shadow_eps;
+            ShadowItem si;
+            si.o[0] = so3.x; si.o[1] = so3.y; si.o[2] = so3.z;
+            si.d[0] = wi.x; si.d[1] = wi.y; si.d[2] = wi.z;
+            si.tmax = dist; si.time = time;
+            W.shadows[path * L + li] = si;
+            ShadowContrib sc;
+            const double NdotL = smax(0.0, dot(N, wi));
+            sc.has = NdotL > 0 ? 1 : 0;
+            sc.pad = 0;
+            if (sc.has) {
+                const double shininess = smax(1.0, M.phong);
+                const V3 Ld = ld3(M.diffuse) * NdotL;
+                const V3 view = normalize(-d);
+                const V3 hv = normalize(wi + view);
+                const double NdotH = smax(0.0, dot(N, hv));
+                const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
+                const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
+                const V3 c = (Ld + Ls) * atten;
+                sc.c[0] = c.x; sc.c[1] = c.y; sc.c[2] = c.z;
+            } else {
+                sc.c[0] = 0.0; sc.c[1] = 0.0; sc.c[2] = 0.0;
+            }
+            W.contrib[path * L + li] = sc;
+        }
         if (BOUNCE && (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && depth < P.max_depth &&
             depth < kMaxDepthGPU) {
             bounce = true;
+            V3 mult;
             if (M.type == RT_MAT_MIRROR) {
                 mult = ld3(M.mirror);
             } else {
                 const double cosI = smax(0.0, -dot(d, N));
                 mult = fresnel_conductor(M.ior, M.absorption_index, cosI) * ld3(M.mirror);
             }
-            rd = normalize(reflect(d, N));
+            V3 rd = normalize(reflect(d, N));
             if (M.roughness != 0.0) {                    // glossy perturbation (:191-197)
                 unsigned long long* rs = W.rng + 2 * path;
                 PCG32 rng(0ull);
@@ -274,102 +430,33 @@ __global__ __launch_bounds__(256) void k_shade(WaveParams W) {
                 rs[0] = rng.state;
                 rs[1] = rng.inc;
             }
-        }
-    }
-    // ---- shadow rays: one per point light (Object+Extension.swift:118-125), compacted
-    const unsigned sbase = wave_append(&W.qcount[kQShadow + depth], nShadow);
-    if (hit) {
-        ShadeOut so;
-        so.lo[0] = Lo.x; so.lo[1] = Lo.y; so.lo[2] = Lo.z;
-        so.first = (int32_t)sbase;
-        so.n = (int32_t)nShadow;
-        W.shade[slot] = so;
-        if (nShadow) {
-            const DMaterial& M = *Mp;
-            for (int li = 0; li < L; ++li) {
-                const DPointLight& PL = P.plights[li];
-                V3 wi = ld3(PL.position) - p;
-                const double dist = length(wi);
-                wi = normalize(wi);
-                const V3 so3 = p + wi * P.shadow_eps;
-                ShadowItem si;
-                si.o[0] = so3.x; si.o[1] = so3.y; si.o[2] = so3.z;
-                si.d[0] = wi.x; si.d[1] = wi.y; si.d[2] = wi.z;
-                si.tmax = dist; si.time = it.time;
-                W.shadows[sbase + li] = si;
-                ShadowContrib sc;
-                const double NdotL = smax(0.0, dot(N, wi));
-                sc.has = NdotL > 0 ? 1 : 0;
-                sc.pad = 0;
-                if (sc.has) {
-                    const double shininess = smax(1.0, M.phong);
-                    const V3 Ld = ld3(M.diffuse) * NdotL;
-                    const V3 view = normalize(-d);
-                    const V3 hv = normalize(wi + view);
-                    const double NdotH = smax(0.0, dot(N, hv));
-                    const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
-                    const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
-                    const V3 c = (Ld + Ls) * atten;
-                    sc.c[0] = c.x; sc.c[1] = c.y; sc.c[2] = c.z;
-                } else {
-                    sc.c[0] = 0.0; sc.c[1] = 0.0; sc.c[2] = 0.0;
-                }
-                W.contrib[sbase + li] = sc;
-            }
-        }
-    }
-    // ---- bounce rays (mirror / conductor), compacted into the next level's queue
-    if (BOUNCE) {
-        const unsigned rbase = wave_append(&W.qcount[kQTrace + depth + 1], bounce ? 1u : 0u);
-        if (bounce) {
             TraceItem nx;
             const V3 no = p + N * P.shadow_eps;
             nx.o[0] = no.x; nx.o[1] = no.y; nx.o[2] = no.z;
             nx.d[0] = rd.x; nx.d[1] = rd.y; nx.d[2] = rd.z;
-            nx.tlo = 0.0; nx.time = it.time; nx.path = path; nx.pad = 0;
-            W.items[(depth + 1) & 1][rbase] = nx;
+            nx.tlo = 0.0; nx.time = time; nx.path = (int32_t)path; nx.pad = 0;
+            W.items[(depth + 1) & 1][path] = nx;
             double* m = W.md + ((size_t)depth * W.P + path) * 3;
             m[0] = mult.x; m[1] = mult.y; m[2] = mult.z;
         }
-        const unsigned long long nb = wave_sum(bounce ? 1ull : 0ull);
-        if (lane_id() == 0 && nb) atomicAdd(&P.counters[1], nb);
+        if (!bounce) W.term[path] = depth;
     }
-    if (hit && !bounce) W.term[path] = depth;
-    const unsigned long long ns = wave_sum((unsigned long long)nShadow);
-    if (lane_id() == 0 && ns) atomicAdd(&P.counters[0], ns);
-    flush_counts(W, cnt, COUNT);
-}
-
-// ---------------------------------------------------------------------- k_shadow
-template <bool COUNT>
-__global__ __launch_bounds__(256) void k_shadow(WaveParams W) {
-    extern __shared__ unsigned long long lds_stack[];
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    Counts cnt{0, 0, 0, 0, 0, 0};
-    if (slot < (int64_t)W.qcount[kQShadow + W.depth]) {
-        const ShadowItem si = W.shadows[slot];
-        Stack st;
-        st.lds = (lds_u64*)(lds_stack + threadIdx.x);
-        st.stride = blockDim.x;
-        st.sp = 0;
-        const bool occ = occluded<COUNT>(W.R, ld3(si.o), ld3(si.d), si.tmax, si.time, st, cnt);
-        W.occluded[slot] = occ ? 1 : 0;
-    }
+    // empty queue entries for the shadow and next-level queues
+    for (int li = (int)nShadow; li < L; ++li) W.shadows[path * L + li].tmax = -1.0;
+    if (BOUNCE && !bounce) W.items[(depth + 1) & 1][path].path = -1;
     flush_counts(W, cnt, COUNT);
 }
 
 // ---------------------------------------------------------------------- k_gather
 __global__ __launch_bounds__(256) void k_gather(WaveParams W) {
     const int depth = W.depth;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t count = depth == 0 ? W.P : (int64_t)W.qcount[kQTrace + depth];
-    if (slot >= count) return;
-    const int32_t path = W.items[depth & 1][slot].path;
-    if (path < 0) return;
-    if (W.hits[slot].inst < 0 || !W.R.has_tlas) return;    // misses were written by k_shade
-    const ShadeOut so = W.shade[slot];
+    const int64_t path = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (path >= W.P) return;
+    if (depth == 0 ? !pixel_of(W, path).valid : W.items[depth & 1][path].path < 0) return;
+    if (W.hits[path].inst < 0 || !W.R.has_tlas) return;     // misses were written by k_shade
+    const ShadeOut so = W.shade[path];
     V3 Lo = ld3(so.lo);
-    for (int l = 0; l < so.n; ++l) {                         // light order, :118-143
+    for (int l = 0; l < so.n; ++l) {                          // light order, :118-143
         const ShadowContrib& c = W.contrib[so.first + l];
         if (c.has && !W.occluded[so.first + l]) Lo = Lo + ld3(c.c);
     }
@@ -466,7 +553,7 @@ int32_t wave_reserve(WaveBuffers& b, int64_t paths, int32_t lights, int32_t dept
     rc |= grow<int32_t>((void**)&b.term, P, by);
     rc |= grow<unsigned long long>((void**)&b.rng, 2 * P, by);
     rc |= grow<double>((void**)&b.accum, 3 * P, by);
-    rc |= grow<unsigned>((void**)&b.qcount, 64, by);
+    rc |= grow<unsigned>((void**)&b.qcount, kCounterSlots * 8, by);
     if (rc != RT_OK) { wave_release(b); return RT_ERR_OOM; }
     b.cap_paths = P; b.cap_lights = L; b.cap_depth = D; b.bytes = by;
     return RT_OK;
@@ -489,30 +576,47 @@ int32_t wave_render(const RenderParams& R, WaveBuffers& b, bool bounce, bool cou
     W.rng = b.rng; W.accum = b.accum; W.qcount = b.qcount;
     W.P = P; W.tilesX = tilesX;
     W.nsamples = R.cam.n * R.cam.n;
+    // Persistent refill traversal (k_persist) is opt-in (MYRT_PERSIST=1): replacing
+    // finished rays mid-flight breaks the 8x8-tile coherence of a wave's node fetches and
+    // measured 2.2x slower than one-ray-per-lane launches on C3 (profiles/r01_v3_*).
+    const char* pe = std::getenv("MYRT_PERSIST");
+    const bool persist = R.identity && R.has_tlas && (pe && pe[0] == '1');
     const dim3 block(256);
     const dim3 gP((unsigned)((P + 255) / 256));
-    const dim3 gS((unsigned)((P * std::max(L, 1) + 255) / 256));
-    const size_t lds = (size_t)kLds * 256 * sizeof(int2);
-    if (hipMemsetAsync(b.qcount, 0, 64 * sizeof(unsigned), stream) != hipSuccess) return RT_ERR_DEVICE;
+    const int64_t NS = P * std::max(L, 1);
+    const dim3 gS((unsigned)((NS + 255) / 256));
+    const dim3 gPersist(256 * 8);                 // >= resident blocks; extra blocks find no work
+    const size_t lds = (size_t)kLds * 256 * sizeof(unsigned long long);
+    // qcount: 8 XCD-homed work counters per traversal launch, fresh block per launch
+    const int launchesPerFrame = W.nsamples * (maxd + 1) * 2;
+    if (launchesPerFrame > kCounterSlots) return RT_ERR_UNSUPPORTED;
+    if (hipMemsetAsync(b.qcount, 0, (size_t)launchesPerFrame * 8 * sizeof(unsigned), stream) != hipSuccess)
+        return RT_ERR_DEVICE;
+    int ctrSlot = 0;
+    auto trace = [&](int mode, int64_t N) {
+        unsigned* ctr = b.qcount + 8 * (ctrSlot++);
+        const dim3 g = mode == 2 ? gS : gP;
+        if (persist) {
+            if (mode == 0) { if (count) hipLaunchKernelGGL((k_persist<true, 0>), gPersist, block, lds, stream, W, N, ctr);
+                             else hipLaunchKernelGGL((k_persist<false, 0>), gPersist, block, lds, stream, W, N, ctr); }
+            if (mode == 1) { if (count) hipLaunchKernelGGL((k_persist<true, 1>), gPersist, block, lds, stream, W, N, ctr);
+                             else hipLaunchKernelGGL((k_persist<false, 1>), gPersist, block, lds, stream, W, N, ctr); }
+            if (mode == 2) { if (count) hipLaunchKernelGGL((k_persist<true, 2>), gPersist, block, lds, stream, W, N, ctr);
+                             else hipLaunchKernelGGL((k_persist<false, 2>), gPersist, block, lds, stream, W, N, ctr); }
+        } else {
+            if (mode == 0) { if (count) hipLaunchKernelGGL((k_general<true, 0>), g, block, lds, stream, W, N);
+                             else hipLaunchKernelGGL((k_general<false, 0>), g, block, lds, stream, W, N); }
+            if (mode == 1) { if (count) hipLaunchKernelGGL((k_general<true, 1>), g, block, lds, stream, W, N);
+                             else hipLaunchKernelGGL((k_general<false, 1>), g, block, lds, stream, W, N); }
+            if (mode == 2) { if (count) hipLaunchKernelGGL((k_general<true, 2>), g, block, lds, stream, W, N);
+                             else hipLaunchKernelGGL((k_general<false, 2>), g, block, lds, stream, W, N); }
+        }
+    };
     for (int s = 0; s < W.nsamples; ++s) {
         W.sample = s;
         for (int dl = 0; dl <= maxd; ++dl) {
             W.depth = dl;
-            if (s > 0 || dl > 0) {
-                // reset this level's queue counters for the new sample (level 0 has none)
-                if (hipMemsetAsync(b.qcount + kQShadow + dl, 0, sizeof(unsigned), stream) != hipSuccess)
-                    return RT_ERR_DEVICE;
-                if (dl + 1 <= maxd &&
-                    hipMemsetAsync(b.qcount + kQTrace + dl + 1, 0, sizeof(unsigned), stream) != hipSuccess)
-                    return RT_ERR_DEVICE;
-            }
-            if (dl == 0) {
-                if (count) hipLaunchKernelGGL((k_trace<true, true>), gP, block, lds, stream, W);
-                else hipLaunchKernelGGL((k_trace<false, true>), gP, block, lds, stream, W);
-            } else {
-                if (count) hipLaunchKernelGGL((k_trace<true, false>), gP, block, lds, stream, W);
-                else hipLaunchKernelGGL((k_trace<false, false>), gP, block, lds, stream, W);
-            }
+            trace(dl == 0 ? 0 : 1, P);
             if (bounce) {
                 if (count) hipLaunchKernelGGL((k_shade<true, true>), gP, block, 0, stream, W);
                 else hipLaunchKernelGGL((k_shade<false, true>), gP, block, 0, stream, W);
@@ -520,10 +624,8 @@ int32_t wave_render(const RenderParams& R, WaveBuffers& b, bool bounce, bool cou
                 if (count) hipLaunchKernelGGL((k_shade<true, false>), gP, block, 0, stream, W);
                 else hipLaunchKernelGGL((k_shade<false, false>), gP, block, 0, stream, W);
             }
-            if (L > 0) {
-                if (count) hipLaunchKernelGGL((k_shadow<true>), gS, block, lds, stream, W);
-                else hipLaunchKernelGGL((k_shadow<false>), gS, block, lds, stream, W);
-            }
+            if (L > 0) trace(2, NS);
+            else ctrSlot++;
             hipLaunchKernelGGL(k_gather, gP, block, 0, stream, W);
         }
         if (count) hipLaunchKernelGGL((k_resolve<true>), gP, block, 0, stream, W);
