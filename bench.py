@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
     p.add_argument("--cache", default=os.path.join(ROOT, "scenes_cache"))
-    p.add_argument("--traffic-json", default="", help="PMC traffic summary (tools/pmc_traffic.py output)")
+    p.add_argument("--traffic-json", default="auto",
+                   help="PMC traffic summary (tools/pmc_traffic.py output); auto = profiles/traffic_<config>.json")
     return p.parse_args()
 
 
@@ -135,23 +136,33 @@ def main():
     value = rays_total / t_max / 1e6
     ms_per_step = t_max * 1e3 / args.steps
 
-    # ---- roofline: algorithmic bytes of this launch / average kernel time
+    # ---- roofline: algorithmic bytes of one launch, counted on the GPU in
+    # the reference's traversal order (rt_render_device_counted; equal to the oracle's tally,
+    # tests/test_gpu_parity.py), divided by the average launch time of the timed frames.
     wc = eng.work_counters(out.data_ptr(), 0, first, step, stream=sptr)
-    alg_bytes = 128 * wc.records_fetched + 80 * wc.tri_tests + 72 * wc.normal_fetches + 24 * wc.pixels
+    alg_bytes = (56 * wc.ref_node_fetches + 72 * wc.ref_tri_tests + 72 * wc.ref_smooth_hits
+                 + 24 * wc.ref_pixels)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
+    traffic, tpath = None, args.traffic_json
+    if tpath == "auto":
+        tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if tpath and os.path.exists(tpath) and world == 1:
         try:
-            with open(args.traffic_json) as fh:
+            with open(tpath) as fh:
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": os.path.relpath(tpath, ROOT) if traffic is not None else None,
                 "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
-                "bytes_per_ray": round(alg_bytes / max(1, rays_rank), 1),
-                "counts": {"records": int(wc.records_fetched), "tri_tests": int(wc.tri_tests),
-                           "normal_fetches": int(wc.normal_fetches), "pixels": int(wc.pixels)}}
+                "alg_bytes_per_ray": round(alg_bytes / max(1, rays_rank), 1),
+                "alg_counts": {"node_fetches": int(wc.ref_node_fetches), "tri_tests": int(wc.ref_tri_tests),
+                               "smooth_hits": int(wc.ref_smooth_hits), "pixels": int(wc.ref_pixels)},
+                "executed": {"records_128B": int(wc.records_fetched), "tri_tests": int(wc.tri_tests),
+                             "normal_fetches": int(wc.normal_fetches), "pixels": int(wc.pixels),
+                             "load_bytes": int(128 * wc.records_fetched + 80 * wc.tri_tests
+                                               + 72 * wc.normal_fetches + 24 * wc.pixels)}}
 
     # ---- CPU baseline (rank 0, N = 1 only): oracle on a bounded sample of the same frame
     cpu = None

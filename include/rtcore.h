@@ -204,6 +204,14 @@ typedef struct rt_work_counters {
     int64_t normal_fetches;     /* 72-B smooth-normal triples loaded (final hits)     */
     int64_t instance_entries;   /* world->local transforms                            */
     int64_t pixels;             /* pixels written                                     */
+    /* The same frame walked in the REFERENCE's order (no t-pruning; any-hit visits L
+     * before R and stops at the first occluder; RTContext.swift:544-829), tallied as
+     * SURVEY.md §8(d) defines algorithmic work: B = 56*N_nodeFetch + 72*N_triTest +
+     * 72*N_smoothHit + 24*N_pixelWrite.  Equal to the oracle's counts (tests/test_gpu_parity.py). */
+    int64_t ref_node_fetches;   /* node bounds loaded (roots + both children of each popped inner node; every any-hit pop) */
+    int64_t ref_tri_tests;      /* Moeller-Trumbore tests                             */
+    int64_t ref_smooth_hits;    /* closer smooth hits (normal triple interpolated)    */
+    int64_t ref_pixels;         /* pixels written                                     */
 } rt_work_counters;
 int32_t rt_render_device_counted(rt_scene* scene, int32_t device_slot, int32_t camera_index,
                                  int32_t chunk_first, int32_t chunk_step,

@@ -95,6 +95,17 @@ struct PCG32 {
     __device__ __forceinline__ double nextFloat() { return (double)next() * 2.3283064365386963e-10; }
 };
 
+// XCD-aware tile order.  Workgroups are dealt to the 8 XCDs round-robin by linear id,
+// and each XCD has its own 4 MB L2: without a remap every XCD renders every 8th tile of
+// the whole image and must cache the whole visible BVH.  With it, XCD x renders the
+// contiguous tile range [x*q + min(x,r), ...) (q = nb/8, r = nb%8), i.e. one band of the
+// image, so its L2 holds only that band's part of the tree.  Bijective on [0, nb).
+__device__ __forceinline__ int xcd_tile(int b, int nb, bool remap) {
+    if (!remap) return b;
+    const int x = b & 7, k = b >> 3, q = nb >> 3, r = nb & 7;
+    return x * q + min(x, r) + k;
+}
+
 // ----------------------------------------------------------------- traversal stack
 // Per-lane stack: the first kLds entries live in LDS ([slot][lane], so each lane hits its
 // own bank), deeper entries spill to a private (scratch) array that lives OUTSIDE the
@@ -145,7 +156,19 @@ struct Stack {
     name.stride = blockDim.x;                                        \
     name.sp = 0
 
-struct Counts { unsigned shadow, secondary; unsigned long long recs, tris, normals, insts; };
+// Work counters (COUNT instantiations only).  recs/tris/normals/insts = work this kernel
+// executed.  With RenderParams::count_ref set, the COUNT walk instead follows the
+// reference's traversal exactly - no t-pruning, any-hit walks L before R - and `nodes` /
+// `smooth` tally its N_nodeFetch / N_smoothHit as SURVEY.md §8(d) defines them (the
+// oracle's Counters, oracle/rt_oracle.cpp intersectBLAS/occludedBLAS).
+struct Counts {
+    unsigned shadow, secondary;
+    unsigned long long recs, tris, normals, insts, nodes, smooth;
+};
+constexpr int kMissRef = 0x7fffffff;   // count_ref any-hit: a pushed child whose slab test missed
+
+// reference-order counting requested (a runtime flag read only by COUNT instantiations)
+#define MYRT_REF(P) (COUNT && (P).count_ref)
 
 struct Hit { double t, u, v; int tri, inst; };
 
@@ -182,22 +205,23 @@ __device__ __forceinline__ bool finite3(const V3& a) {
 
 // Closest-hit triangle test, intersectTriangle (RTContext.swift:479-510) minus the
 // hit-point/normal writes, which are recomputed once for the final hit (same values).
-__device__ __forceinline__ void tri_closest(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double eps,
+__device__ __forceinline__ bool tri_closest(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double eps,
                                            Hit& h, int triIdx, int instIdx) {
     const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
     const V3 pvec = cross(d, e2);
     const double det = dot(e1, pvec);
-    if (fabs(det) < eps) return;
+    if (fabs(det) < eps) return false;
     const double invDet = 1.0 / det;
     const V3 tvec = o_mb - v0;
     const double u = dot(tvec, pvec) * invDet;
-    if (u < 0.0 || u > 1.0) return;
+    if (u < 0.0 || u > 1.0) return false;
     const V3 q = cross(tvec, e1);
     const double v = dot(d, q) * invDet;
-    if (v < 0.0 || u + v > 1.0) return;
+    if (v < 0.0 || u + v > 1.0) return false;
     const double t = dot(e2, q) * invDet;
-    if (t <= smax(eps, tlo) || t >= h.t) return;
+    if (t <= smax(eps, tlo) || t >= h.t) return false;
     h.t = t; h.u = u; h.v = v; h.tri = triIdx; h.inst = instIdx;
+    return true;
 }
 // triShadowHit (RTContext.swift:832-848)
 __device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double thi,
@@ -221,7 +245,7 @@ __device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, cons
 // (true), or the caller must pop (false).  Order = near first, ties to L (the reference
 // pushes R then L after `if d1 > d2 swap`, RTContext.swift:600-606); the far child is
 // pushed.  Children beyond `lim` (conservative t-pruning) count as misses.
-template <bool COUNT, bool FAST>
+template <bool COUNT, bool FAST, bool SHADOW>
 __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
                                            Stack& st, Counts& c) {
     const WRec& R = P.recs[ref];
@@ -232,6 +256,18 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
     h0 = h0 && !(t0 > lim);
     h1 = h1 && !(t1 > lim);
     const int a = R.ref[0], b = R.ref[1];
+    if (MYRT_REF(P)) {
+        if (!SHADOW) {
+            c.nodes += 2;                    // intersectBLAS loads both children (RTContext.swift:600-606)
+        } else {
+            // occludedBLAS pushes R then L unconditionally and tests each on pop
+            // (RTContext.swift:818-826): L is popped next (+1); R - or a miss marker - waits.
+            c.nodes += 1;
+            st.push(h1 ? b : kMissRef, t1);
+            if (h0) { ref = a; return true; }
+            return false;
+        }
+    }
     if (h0 && h1) {
         const bool sw = t0 > t1;
         st.push(sw ? a : b, sw ? t0 : t1);
@@ -245,10 +281,15 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
 
 // Pop the next node whose entry distance does not exceed `lim`; false when the stack
 // (down to `base`) is exhausted.
-__device__ __forceinline__ bool pop_next(Stack& st, int base, double lim, int& ref) {
+template <bool COUNT, bool SHADOW>
+__device__ __forceinline__ bool pop_next(const RenderParams& P, Stack& st, int base, double lim, int& ref, Counts& c) {
     while (st.sp > base) {
         double tlo;
         const int r = st.pop(tlo);
+        if (SHADOW && MYRT_REF(P)) {         // every pop is a node fetch of occludedBLAS
+            c.nodes += 1;
+            if (r == kMissRef) continue;
+        }
         if (tlo > lim) continue;
         ref = r;
         return true;
@@ -260,23 +301,23 @@ __device__ __forceinline__ bool pop_next(Stack& st, int base, double lim, int& r
 // node the caller has already tested (the root); children are tested at the parent
 // (one 128-B record holds both).  LEAF(ref) handles a leaf run and returns true to
 // terminate the walk (any-hit).  LIMIT() gives the current pruning distance.
-template <bool COUNT, bool FAST, class Leaf, class Limit>
+template <bool COUNT, bool FAST, bool SHADOW, class Leaf, class Limit>
 __device__ __forceinline__ bool walk(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st, int base,
                                      Counts& c, Leaf leaf, Limit limit) {
     for (;;) {
         if (ref >= 0) {
-            if (inner_step<COUNT, FAST>(P, ref, o, inv, limit(), st, c)) continue;
+            if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, limit(), st, c)) continue;
         } else {
             if (leaf(ref)) return true;
         }
-        if (!pop_next(st, base, limit(), ref)) return false;
+        if (!pop_next<COUNT, SHADOW>(P, st, base, limit(), ref, c)) return false;
     }
 }
-template <bool COUNT, class Leaf, class Limit>
+template <bool COUNT, bool SHADOW, class Leaf, class Limit>
 __device__ __forceinline__ bool walk_any(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st,
                                          int base, Counts& c, Leaf leaf, Limit limit) {
-    if (__all(finite3(inv))) return walk<COUNT, true>(P, ref, o, inv, st, base, c, leaf, limit);
-    return walk<COUNT, false>(P, ref, o, inv, st, base, c, leaf, limit);
+    if (__all(finite3(inv))) return walk<COUNT, true, SHADOW>(P, ref, o, inv, st, base, c, leaf, limit);
+    return walk<COUNT, false, SHADOW>(P, ref, o, inv, st, base, c, leaf, limit);
 }
 
 template <bool COUNT>
@@ -284,7 +325,9 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
                                   double time, Hit& h, Stack& st, Counts& c) {
     const double eps = P.eps;
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-    auto limit = [&]() { return h.t * P.prune_rel + P.prune_abs; };   // prune_rel = 1 + delta
+    // prune_rel = 1 + delta; reference-order counting walks without pruning
+    auto limit = [&]() { return MYRT_REF(P) ? DINF : h.t * P.prune_rel + P.prune_abs; };
+    if (MYRT_REF(P)) c.nodes += 1;           // the TLAS root's bounds (RTContext.swift:642)
     double d0;
     if (!slab_hit<false>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
                          P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps, d0))
@@ -294,6 +337,7 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
             const DTlasLeafEntry le = P.tlas_leaf[e];
             const DInstance& I = P.insts[le.inst];
             if (COUNT) c.insts++;
+            if (MYRT_REF(P)) c.nodes += 1;   // the BLAS root's bounds (RTContext.swift:550-552)
             // world -> local (RTContext.swift:657-673)
             const V3 instOffset = ld3(I.motion) * time;
             const V3 ow = o - instOffset;
@@ -309,14 +353,15 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
                     for (int t = ~r;; ++t) {
                         const TriRec& T = P.tris[t];
                         if (COUNT) c.tris++;
-                        tri_closest(T, omb, dl, tlo, eps, h, t, inst);
+                        const bool closer = tri_closest(T, omb, dl, tlo, eps, h, t, inst);
+                        if (MYRT_REF(P) && closer && I.smooth) c.smooth++;
                         if (T.last) break;
                     }
                     return false;
                 };
                 const int sbase = st.sp;
                 if (I.root_ref < 0) blas_leaf(I.root_ref);
-                else walk_any<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+                else walk_any<COUNT, false>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
             }
             if (le.last) break;
         }
@@ -324,7 +369,7 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
     };
     const int base = st.sp;
     if (P.tlas_root_ref < 0) tlas_leaf(P.tlas_root_ref);
-    else walk_any<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+    else walk_any<COUNT, false>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
 }
 
 template <bool COUNT>
@@ -333,8 +378,9 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
     if (!P.has_tlas) return false;
     const double eps = P.eps;
     const V3 inv = rcp(d);
-    const double lim = tmax * P.prune_rel + P.prune_abs;
+    const double lim = MYRT_REF(P) ? DINF : tmax * P.prune_rel + P.prune_abs;
     auto limit = [&]() { return lim; };
+    if (MYRT_REF(P)) c.nodes += 1;           // occludedTLAS pops the root (RTContext.swift:727-731)
     double d0;
     if (!slab_hit<false>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2], P.tlas_root_hi[0],
                          P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv, eps, d0) || d0 > lim)
@@ -344,6 +390,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
             const DTlasLeafEntry le = P.tlas_leaf[e];
             const DInstance& I = P.insts[le.inst];
             if (COUNT) c.insts++;
+            if (MYRT_REF(P)) c.nodes += 1;   // occludedBLAS pops its root (RTContext.swift:789-793)
             const V3 instOffset = ld3(I.motion) * time;
             const V3 ol = m4_point(I.w2l, o - instOffset, 1.0);
             const V3 dl = m4_point(I.w2l, d, 0.0);
@@ -364,7 +411,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
                 const int sbase = st.sp;
                 bool hit;
                 if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
-                else hit = walk_any<COUNT>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
+                else hit = walk_any<COUNT, true>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
                 if (hit) { st.sp = sbase; return true; }
             }
             if (le.last) break;
@@ -374,7 +421,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
     const int base = st.sp;
     bool hit;
     if (P.tlas_root_ref < 0) hit = tlas_leaf(P.tlas_root_ref);
-    else hit = walk_any<COUNT>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
+    else hit = walk_any<COUNT, true>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
     st.sp = base;
     return hit;
 }
@@ -392,7 +439,7 @@ __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Sta
                                             const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
     const double eps = P.eps;
     if (ref >= 0) {
-        if (inner_step<COUNT, FAST>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c))
+        if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c))
             return 0;
     } else {
         const int e = ~ref;
@@ -422,7 +469,7 @@ __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Sta
             }
         }
     }
-    return pop_next(st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref) ? 0 : 1;
+    return pop_next<COUNT, SHADOW>(P, st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref, c) ? 0 : 1;
 }
 
 // Root test of the unified walk (the TLAS root is popped and tested first,
@@ -434,6 +481,43 @@ __device__ __forceinline__ bool unified_begin(const RenderParams& P, const V3& o
         return false;
     ref = P.tlas_root_ref;
     return true;
+}
+
+// Whole-ray unified walks (identity scenes): closest hit and any hit with one stack.
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
+                                                 double tlo, Hit& h, Stack& st, Counts& c) {
+    int ref;
+    if (!unified_begin(P, o, inv, DINF, ref)) return;   // the stack is empty here (base 0)
+    while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0) {}
+}
+template <bool COUNT>
+__device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
+                                            double tlo, Hit& h, Stack& st, Counts& c) {
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    if (__all(finite3(inv))) uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
+    else uni_closest_walk<COUNT, false>(P, o, d, inv, tlo, h, st, c);
+}
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
+                                                  double tmax, Stack& st, Counts& c) {
+    int ref;
+    if (!unified_begin(P, o, inv, tmax * P.prune_rel + P.prune_abs, ref)) return false;
+    Hit h;   // unused by any-hit steps
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    const int base = st.sp;
+    int r;
+    while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0) {}
+    st.sp = base;
+    return r == 2;
+}
+template <bool COUNT>
+__device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o, const V3& d, double tmax,
+                                             Stack& st, Counts& c) {
+    if (!P.has_tlas) return false;
+    const V3 inv = rcp(d);
+    if (__all(finite3(inv))) return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
+    return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);
 }
 
 // orthonormalBasis (Object+Extension.swift:531-552)

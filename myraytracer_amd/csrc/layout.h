@@ -91,12 +91,15 @@ struct RenderParams {
     int32_t max_depth;
     int32_t chunk_first, chunk_step, num_chunks;   // selected 8-row chunks
     int32_t stack_depth;             // LDS stack entries per lane
-    int32_t pad0;
+    int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
+    int32_t xcd_remap;               // megakernel: give each XCD a contiguous band of tiles (L2 locality)
+    int32_t pad1;
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
-    unsigned long long* counters;    // [0] shadow rays, [1] secondary rays, [2..6] work counters
+    unsigned long long* counters;    // [0] shadow rays, [1] secondary rays, [2..8] work counters (kCounterWords)
 };
 
+constexpr int kCounterWords = 16;   // u64 words behind RenderParams::counters
 constexpr int kMaxDepthGPU = 16;     // mirror/conductor recursion levels kept per lane
 
 }  // namespace myrt

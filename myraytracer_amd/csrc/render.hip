@@ -36,7 +36,7 @@ namespace dev {
 // trace() (Object+Extension.swift:96-283) for diffuse/mirror/conductor materials and
 // point lights.  The recursion Lo + M*trace(depth+1) is run forward and combined
 // backward with the same per-level NaN guard, so the result is the recursive one.
-template <bool COUNT, bool BOUNCE>
+template <bool COUNT, bool BOUNCE, bool UNI>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
                          Counts& c) {
     V3 Lst[BOUNCE ? kMaxDepthGPU : 1], Mst[BOUNCE ? kMaxDepthGPU : 1];
@@ -46,7 +46,8 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         if (!P.has_tlas) { L = v3(0, 0, 0); break; }
         const V3 inv = rcp(d);
         Hit h;
-        intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
+        if (UNI) uni_closest<COUNT>(P, o, d, inv, tlo, h, st, c);
+        else intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
         if (h.inst < 0) { L = ld3(P.background); break; }
         // reconstruct the hit exactly as intersectTriangle + intersectTLAS wrote it
         const TriRec& T = P.tris[h.tri];
@@ -79,7 +80,8 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 wi = normalize(wi);
                 const V3 so = p + wi * P.shadow_eps;
                 c.shadow++;
-                const bool blocked = occluded<COUNT>(P, so, wi, dist, time, st, c);
+                const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
+                                         : occluded<COUNT>(P, so, wi, dist, time, st, c);
                 if (!blocked) {
                     const double NdotL = smax(0.0, dot(N, wi));
                     if (NdotL > 0) {
@@ -135,19 +137,31 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 
 
 // One block = 256 lanes = 4 waves; each wave renders an 8x8 tile of one 8-row chunk.
-template <bool COUNT, bool BOUNCE>
-__global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
+#ifndef MYRT_MEGA_WPE
+#define MYRT_MEGA_WPE 0      // tuning knob: amdgpu_waves_per_eu for the megakernel (0 = compiler's choice)
+#endif
+#if MYRT_MEGA_WPE > 0
+#define MYRT_MEGA_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_MEGA_WPE)))
+#else
+#define MYRT_MEGA_ATTR
+#endif
+// UNI: identity scenes walk TLAS + BLAS as one tree (device.h unified_step).
+template <bool COUNT, bool BOUNCE, bool UNI>
+__global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int i = blockIdx.x * 32 + wave * 8 + (lane & 7);
-    const int slot = blockIdx.y;                       // position in the selected chunk list
+    // one tile = 32x8 pixels of one selected chunk; tiles are row-major over (slot, column)
+    const int gx = (P.cam.width + 31) >> 5;
+    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap != 0);
+    const int i = (tile % gx) * 32 + wave * 8 + (lane & 7);
+    const int slot = tile / gx;                        // position in the selected chunk list
     const int chunk = P.chunk_first + slot * P.chunk_step;
     const int rowInChunk = lane >> 3;
     const int j = chunk * 8 + rowInChunk;
     const DCamera& C = P.cam;
     const bool valid = (i < C.width) && (j < C.height);
-    Counts cnt{0, 0, 0, 0, 0, 0};
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
     if (valid) {
         MYRT_STACK(st, lds_stack);
         PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
@@ -185,7 +199,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
                 const double denom = dot(dir, w);
                 const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
                 const double tlo = smax(tImg, 0.0);
-                const V3 col = trace_path<COUNT, BOUNCE>(P, camEye, dir, tlo, time, rng, st, cnt);
+                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt);
                 pixel = pixel + col;
                 sampleIndex += 1;
                 if (sampleIndex >= C.samples) break;
@@ -220,6 +234,8 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
             atomicAdd(&P.counters[2], a); atomicAdd(&P.counters[3], b); atomicAdd(&P.counters[4], cc);
             atomicAdd(&P.counters[5], dd); atomicAdd(&P.counters[6], ee);
         }
+        const unsigned long long ff = wave_sum(cnt.nodes), gg = wave_sum(cnt.smooth);
+        if (lane == 0 && P.count_ref) { atomicAdd(&P.counters[7], ff); atomicAdd(&P.counters[8], gg); }
     }
 }
 
@@ -249,7 +265,7 @@ struct DeviceReplica {
     DTlasLeafEntry* tlas_leaf = nullptr;
     DMaterial* mats = nullptr;
     DPointLight* plights = nullptr;
-    unsigned long long* counters = nullptr;   // 8 x u64
+    unsigned long long* counters = nullptr;   // kCounterWords x u64
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int64_t bytes = 0;
@@ -296,7 +312,7 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r) {
     if ((rc = upload(S.tlas_leaf, &r.tlas_leaf, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.mats, &r.mats, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.plights, &r.plights, r.bytes)) != RT_OK) return rc;
-    HIP_TRY(hipMalloc((void**)&r.counters, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&r.counters, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
@@ -394,6 +410,10 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     for (int32_t c = first; c < num_chunks_total(P.cam.height); c += step) nsel++;
     P.num_chunks = nsel;
     P.stack_depth = dev::kLds;
+    {
+        const char* xe = std::getenv("MYRT_XCD");                // A/B switch: MYRT_XCD=0
+        P.xcd_remap = (xe && xe[0] == '0') ? 0 : 1;
+    }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
     return P;
@@ -413,24 +433,29 @@ static bool use_megakernel() {
 
 static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {
     if (P.num_chunks == 0) return RT_OK;
-    if (!use_megakernel()) {
+    if (!use_megakernel() && !P.count_ref) {   // reference-order counting is a megakernel mode
         const bool bounce_w = scene_has_bounce(s->host) && P.max_depth > 0;
         const int32_t rc = wave_render(P, r.wave, bounce_w, count, stream);
         if (rc != RT_OK) return fail(rc, rc == RT_ERR_OOM ? "device allocation of wavefront queues failed"
                                                          : "wavefront launch failed");
         return RT_OK;
     }
-    dim3 grid((unsigned)((P.cam.width + 31) / 32), (unsigned)P.num_chunks, 1);
+    dim3 grid((unsigned)(((P.cam.width + 31) / 32) * P.num_chunks), 1, 1);
     dim3 block(256, 1, 1);
     const size_t lds = (size_t)dev::kLds * 256 * sizeof(int2);
     const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
+    // the unified walk needs an identity scene; reference-order counting uses the general walk
+    const char* ue = std::getenv("MYRT_UNIFIED");
+    const bool uni = P.identity && P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
+#define MYRT_LAUNCH(C_, B_, U_) hipLaunchKernelGGL((dev::render_kernel<C_, B_, U_>), grid, block, lds, stream, P)
     if (count) {
-        if (bounce) hipLaunchKernelGGL((dev::render_kernel<true, true>), grid, block, lds, stream, P);
-        else hipLaunchKernelGGL((dev::render_kernel<true, false>), grid, block, lds, stream, P);
+        if (bounce) { if (uni) MYRT_LAUNCH(true, true, true); else MYRT_LAUNCH(true, true, false); }
+        else { if (uni) MYRT_LAUNCH(true, false, true); else MYRT_LAUNCH(true, false, false); }
     } else {
-        if (bounce) hipLaunchKernelGGL((dev::render_kernel<false, true>), grid, block, lds, stream, P);
-        else hipLaunchKernelGGL((dev::render_kernel<false, false>), grid, block, lds, stream, P);
+        if (bounce) { if (uni) MYRT_LAUNCH(false, true, true); else MYRT_LAUNCH(false, true, false); }
+        else { if (uni) MYRT_LAUNCH(false, false, true); else MYRT_LAUNCH(false, false, false); }
     }
+#undef MYRT_LAUNCH
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -505,7 +530,7 @@ int32_t rt_render_device(rt_scene* s, int32_t slot, int32_t cam, int32_t first, 
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
-    HIP_TRY(hipMemsetAsync(r.counters, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
     RenderParams P = make_params(s, r, cam, first, step, d_rgb, d_rgba8);
     return launch(s, r, P, st, false);
 }
@@ -515,7 +540,7 @@ int32_t rt_stats_collect(rt_scene* s, int32_t slot, rt_stats* stats) {
     if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
-    unsigned long long c[8];
+    unsigned long long c[kCounterWords];
     HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
     if (stats) { stats->shadow_rays = (int64_t)c[0]; stats->secondary_rays = (int64_t)c[1]; }
     return RT_OK;
@@ -530,16 +555,25 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
-    HIP_TRY(hipMemsetAsync(r.counters, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
     RenderParams P = make_params(s, r, cam, first, step, d_rgb, nullptr);
+    rc = launch(s, r, P, st, true);                  // 1) work this path executes
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    unsigned long long c[kCounterWords];
+    HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
+    P.count_ref = 1;                                 // 2) the reference's work
     rc = launch(s, r, P, st, true);
     if (rc != RT_OK) return rc;
     HIP_TRY(hipStreamSynchronize(st));
-    unsigned long long c[8];
-    HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
+    unsigned long long q[kCounterWords];
+    HIP_TRY(hipMemcpy(q, r.counters, sizeof(q), hipMemcpyDeviceToHost));
     if (out) {
         out->records_fetched = (int64_t)c[2]; out->tri_tests = (int64_t)c[3]; out->normal_fetches = (int64_t)c[4];
         out->instance_entries = (int64_t)c[5]; out->pixels = (int64_t)c[6];
+        out->ref_node_fetches = (int64_t)q[7]; out->ref_tri_tests = (int64_t)q[3];
+        out->ref_smooth_hits = (int64_t)q[8]; out->ref_pixels = (int64_t)q[6];
     }
     return RT_OK;
 }
@@ -577,7 +611,7 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
             double* d_rgb = nullptr; uint8_t* d_rgba = nullptr;
             HIP_TRY(hipMalloc((void**)&d_rgb, (size_t)rows * W * 3 * sizeof(double)));
             if (out_rgba8) HIP_TRY(hipMalloc((void**)&d_rgba, (size_t)rows * W * 4));
-            HIP_TRY(hipMemsetAsync(r.counters, 0, 8 * sizeof(unsigned long long), r.stream));
+            HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
             RenderParams P = make_params(s, r, cam, myFirst, myStep, d_rgb, d_rgba);
             HIP_TRY(hipEventRecord(r.ev0, r.stream));
             int32_t lrc = launch(s, r, P, r.stream, false);
@@ -587,7 +621,7 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
             std::vector<uint8_t> h_rgba(out_rgba8 ? (size_t)rows * W * 4 : 0);
             HIP_TRY(hipMemcpyAsync(h_rgb.data(), d_rgb, h_rgb.size() * sizeof(double), hipMemcpyDeviceToHost, r.stream));
             if (out_rgba8) HIP_TRY(hipMemcpyAsync(h_rgba.data(), d_rgba, h_rgba.size(), hipMemcpyDeviceToHost, r.stream));
-            unsigned long long c[8];
+            unsigned long long c[kCounterWords];
             HIP_TRY(hipMemcpyAsync(c, r.counters, sizeof(c), hipMemcpyDeviceToHost, r.stream));
             HIP_TRY(hipStreamSynchronize(r.stream));
             float ms = 0; (void)hipEventElapsedTime(&ms, r.ev0, r.ev1);

@@ -39,14 +39,15 @@ def load_library() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("MYRT_LIB") or LIB_PATH      # MYRT_LIB: A/B a tuning variant (tools/build_variants.sh)
+    if not os.path.exists(path):
         raise RenderError(A.RT_ERR_NO_RENDERER,
-                          f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+                          f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
     try:
         import torch  # noqa: F401  (shared HIP runtime)
     except Exception:  # pragma: no cover - torch is part of the image
         pass
-    _lib = A.bind(C.CDLL(LIB_PATH))
+    _lib = A.bind(C.CDLL(path))
     return _lib
 
 

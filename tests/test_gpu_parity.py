@@ -174,3 +174,42 @@ def test_device_path_matches_host_path():
     assert np.array_equal(out.cpu().numpy(), host)
     wc = eng.work_counters(out.data_ptr(), 0, 0, 1, stream=stream.cuda_stream)
     assert wc.pixels == 200 * 120 and wc.records_fetched > 0 and wc.tri_tests > 0
+
+
+def _ref_counts_case(name):
+    if name == "c2":
+        return scenes.scaled(scenes.scene_c2(inline=True), 160, 120), 0, 1
+    if name == "c3":
+        return scenes.scene_c3(inline=True), 2, 23
+    if name == "instances":
+        sc = scenes.scaled(scenes.scene_c2(inline=True), 96, 64)
+        base = sc.objects[0]
+        sc.objects = [base,
+                      M.MeshInstance(id=11, base_mesh_id=base.id, material="1", transform=M.translation(1.5, 0.0, -1.0)),
+                      M.Triangle(vertices=((-3, -1, -3), (3, -1, -3), (0, 2, -3.5)), material="1")]
+        return sc, 0, 1
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 96, 64)      # mirror bounces
+    sc.materials[0].type = "mirror"
+    sc.materials[0].mirror = (0.5, 0.5, 0.5)
+    sc.max_recursion_depth = 3
+    return sc, 0, 1
+
+
+@pytest.mark.parametrize("case", ["c2", "c3", "instances", "mirror"])
+def test_reference_order_work_counts_match_oracle(case, render_path):
+    """The GPU's reference-order tally (the roofline's algorithmic bytes)
+    equals the oracle's instrumented counts exactly."""
+    import torch
+    if render_path != "mega":
+        pytest.skip("counting launch is path-independent (always the megakernel)")
+    sc, first, step = _ref_counts_case(case)
+    eng = M.RayTracerEngine(sc)
+    W, H = sc.cameras[0].image_resolution
+    rows = M.rows_for_chunks(H, first, step)
+    out = torch.empty((rows, W, 3), dtype=torch.float64, device="cuda")
+    wc = eng.work_counters(out.data_ptr(), 0, first, step)
+    _, ost = oracle.OracleScene(sc).render(0, first, step, threads=0)
+    got = (wc.ref_node_fetches, wc.ref_tri_tests, wc.ref_smooth_hits, wc.ref_pixels)
+    want = (ost.node_fetches, ost.tri_tests, ost.smooth_hits, ost.pixels)
+    assert got == want
+    assert wc.records_fetched > 0 and wc.pixels == wc.ref_pixels
