@@ -95,15 +95,19 @@ struct PCG32 {
     __device__ __forceinline__ double nextFloat() { return (double)next() * 2.3283064365386963e-10; }
 };
 
-// XCD-aware tile order.  Workgroups are dealt to the 8 XCDs round-robin by linear id,
-// and each XCD has its own 4 MB L2: without a remap every XCD renders every 8th tile of
-// the whole image and must cache the whole visible BVH.  With it, XCD x renders the
-// contiguous tile range [x*q + min(x,r), ...) (q = nb/8, r = nb%8), i.e. one band of the
-// image, so its L2 holds only that band's part of the tree.  Bijective on [0, nb).
-__device__ __forceinline__ int xcd_tile(int b, int nb, bool remap) {
-    if (!remap) return b;
-    const int x = b & 7, k = b >> 3, q = nb >> 3, r = nb & 7;
-    return x * q + min(x, r) + k;
+// XCD-aware tile order.  Workgroups are dealt to the 8 XCDs round-robin by linear id
+// and each XCD has its own 4 MB L2.  Identity order gives XCD x every 8th tile; with
+// group size G > 1 XCD x gets runs of G consecutive tiles instead (tile groups dealt
+// round-robin), so neighbouring tiles - which walk the same BVH nodes - share one L2,
+// while every XCD still samples the whole image (whole-band splits are badly
+// imbalanced: sky rows cost a fraction of terrain rows).  Bijective on [0, nb): the
+// tail beyond the last full 8*G round keeps identity order.
+__device__ __forceinline__ int xcd_tile(int b, int nb, int G) {
+    if (G <= 1) return b;
+    const int round = 8 * G, full = nb / round * round;
+    if (b >= full) return b;
+    const int x = b & 7, k = b >> 3;
+    return ((k / G) * 8 + x) * G + (k % G);
 }
 
 // ----------------------------------------------------------------- traversal stack

@@ -92,7 +92,7 @@ struct RenderParams {
     int32_t chunk_first, chunk_step, num_chunks;   // selected 8-row chunks
     int32_t stack_depth;             // LDS stack entries per lane
     int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
-    int32_t xcd_remap;               // megakernel: give each XCD a contiguous band of tiles (L2 locality)
+    int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
     int32_t pad1;
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;

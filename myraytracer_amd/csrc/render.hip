@@ -80,20 +80,26 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 wi = normalize(wi);
                 const V3 so = p + wi * P.shadow_eps;
                 c.shadow++;
-                const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
-                                         : occluded<COUNT>(P, so, wi, dist, time, st, c);
-                if (!blocked) {
-                    const double NdotL = smax(0.0, dot(N, wi));
-                    if (NdotL > 0) {
-                        const double shininess = smax(1.0, M.phong);
-                        const V3 Ld = ld3(M.diffuse) * NdotL;
-                        const V3 view = normalize(-d);
-                        const V3 hv = normalize(wi + view);
-                        const double NdotH = smax(0.0, dot(N, hv));
-                        const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
-                        const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
-                        Lo = Lo + (Ld + Ls) * atten;
-                    }
+                // The contribution is formed before the shadow walk (same expressions, same
+                // values) so that only it - not N, wi, view, material - stays live across
+                // the walk.  With !(NdotL > 0) the reference discards the occlusion result
+                // (:126-141), so the walk is skipped; the ray is still counted as cast.
+                const double NdotL = smax(0.0, dot(N, wi));
+                V3 contrib = v3(0, 0, 0);
+                if (NdotL > 0) {
+                    const double shininess = smax(1.0, M.phong);
+                    const V3 Ld = ld3(M.diffuse) * NdotL;
+                    const V3 view = normalize(-d);
+                    const V3 hv = normalize(wi + view);
+                    const double NdotH = smax(0.0, dot(N, hv));
+                    const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
+                    const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
+                    contrib = (Ld + Ls) * atten;
+                }
+                if (NdotL > 0 || MYRT_REF(P)) {
+                    const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
+                                             : occluded<COUNT>(P, so, wi, dist, time, st, c);
+                    if (!blocked && NdotL > 0) Lo = Lo + contrib;
                 }
             }
         }
@@ -138,7 +144,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 
 // One block = 256 lanes = 4 waves; each wave renders an 8x8 tile of one 8-row chunk.
 #ifndef MYRT_MEGA_WPE
-#define MYRT_MEGA_WPE 0      // tuning knob: amdgpu_waves_per_eu for the megakernel (0 = compiler's choice)
+#define MYRT_MEGA_WPE 4      // amdgpu_waves_per_eu for the megakernel (0 = compiler default = 2 waves at ~200 VGPRs)
 #endif
 #if MYRT_MEGA_WPE > 0
 #define MYRT_MEGA_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_MEGA_WPE)))
@@ -153,7 +159,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     const int wave = tid >> 6, lane = tid & 63;
     // one tile = 32x8 pixels of one selected chunk; tiles are row-major over (slot, column)
     const int gx = (P.cam.width + 31) >> 5;
-    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap != 0);
+    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
     const int i = (tile % gx) * 32 + wave * 8 + (lane & 7);
     const int slot = tile / gx;                        // position in the selected chunk list
     const int chunk = P.chunk_first + slot * P.chunk_step;
@@ -411,8 +417,8 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.num_chunks = nsel;
     P.stack_depth = dev::kLds;
     {
-        const char* xe = std::getenv("MYRT_XCD");                // A/B switch: MYRT_XCD=0
-        P.xcd_remap = (xe && xe[0] == '0') ? 0 : 1;
+        const char* xe = std::getenv("MYRT_XCD");                // tile-group size per XCD (device.h xcd_tile)
+        P.xcd_remap = xe ? std::atoi(xe) : 0;
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
