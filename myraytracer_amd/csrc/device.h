@@ -245,6 +245,57 @@ __device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, cons
     return (t > smax(eps, tlo) && t < thi);
 }
 
+// intersectSphere / intersectPlane (RTContext.swift:513-538) and sphereShadowHit /
+// planeShadowHit (:851-870) on the instance-local ray.  T encodes the primitive
+// (layout.h kPrimSphere / kPrimPlane).
+__device__ __forceinline__ bool prim_closest(int kind, const TriRec& T, const V3& o, const V3& d, double tlo,
+                                             double eps, double& ht) {
+    double t;
+    if (kind == kPrimSphere) {
+        const V3 oc = o - ld3(T.v0);
+        const double rad = T.e1[0];
+        const double a = dot(d, d);
+        const double b = 2.0 * dot(oc, d);
+        const double c = dot(oc, oc) - rad * rad;
+        const double disc = b * b - (4.0 * a) * c;
+        if (disc < 0) return false;
+        const double sd = dsqrt(disc);
+        t = (-b - sd) / (2.0 * a);
+        if (t < eps) t = (-b + sd) / (2.0 * a);
+    } else {
+        const V3 nrm = ld3(T.e1);
+        const double denom = dot(nrm, d);
+        if (fabs(denom) < eps) return false;
+        t = dot(ld3(T.v0) - o, nrm) / denom;
+    }
+    if (t <= smax(eps, tlo) || t >= ht) return false;
+    ht = t;
+    return true;
+}
+__device__ __forceinline__ bool prim_shadow(int kind, const TriRec& T, const V3& o, const V3& d, double thi,
+                                            double eps) {
+    const double tmin = smax(eps, 0.0);                       // shadow rays keep the Ray default tMin = 0
+    double t;
+    if (kind == kPrimSphere) {
+        const V3 oc = o - ld3(T.v0);
+        const double rad = T.e1[0];
+        const double a = dot(d, d);
+        const double b = 2.0 * dot(oc, d);
+        const double c = dot(oc, oc) - rad * rad;
+        const double disc = b * b - (4.0 * a) * c;
+        if (disc < 0) return false;
+        const double sd = dsqrt(disc);
+        t = (-b - sd) / (2.0 * a);
+        if (t < tmin) t = (-b + sd) / (2.0 * a);
+    } else {
+        const V3 nrm = ld3(T.e1);
+        const double denom = dot(nrm, d);
+        if (fabs(denom) < eps) return false;
+        t = dot(ld3(T.v0) - o, nrm) / denom;
+    }
+    return t > tmin && t < thi;
+}
+
 // Test both children of inner record `ref`.  On return `ref` is the next node to visit
 // (true), or the caller must pop (false).  Order = near first, ties to L (the reference
 // pushes R then L after `if d1 > d2 swap`, RTContext.swift:600-606); the far child is
@@ -364,7 +415,12 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
                     return false;
                 };
                 const int sbase = st.sp;
-                if (I.root_ref < 0) blas_leaf(I.root_ref);
+                if (I.kind != kPrimTriangles) {                           // sphere / plane instance
+                    double ht = h.t;
+                    if (prim_closest(I.kind, P.tris[~I.root_ref], ol, dl, tlo, eps, ht)) {
+                        h.t = ht; h.tri = ~I.root_ref; h.inst = inst;
+                    }
+                } else if (I.root_ref < 0) blas_leaf(I.root_ref);
                 else walk_any<COUNT, false>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
             }
             if (le.last) break;
@@ -414,7 +470,8 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
                 };
                 const int sbase = st.sp;
                 bool hit;
-                if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
+                if (I.kind != kPrimTriangles) hit = prim_shadow(I.kind, P.tris[~I.root_ref], ol, dl, tmax, eps);
+                else if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
                 else hit = walk_any<COUNT, true>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
                 if (hit) { st.sp = sbase; return true; }
             }
@@ -522,6 +579,37 @@ __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o,
     const V3 inv = rcp(d);
     if (__all(finite3(inv))) return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
     return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);
+}
+
+// The hit record intersectTriangle/Sphere/Plane + intersectTLAS leave behind
+// (RTContext.swift:479-538, 674-705), rebuilt once for the final (t, tri, u, v, inst):
+// world hit point and the normalized, det-signed world geometric normal.
+template <bool COUNT>
+__device__ __forceinline__ void hit_geometry(const RenderParams& P, const V3& o, const V3& d, double time,
+                                             const Hit& h, V3& p, V3& Ngeo, Counts& c) {
+    const TriRec& T = P.tris[h.tri];
+    const DInstance& I = P.insts[h.inst];
+    V3 nl, pl;
+    if (I.kind == kPrimTriangles) {
+        const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+        if (I.smooth) {
+            if (COUNT) c.normals++;
+            const double* nn = P.normals + (size_t)h.tri * 9;
+            const double w = 1.0 - h.u - h.v;
+            nl = normalize(((w * ld3(nn)) + (h.u * ld3(nn + 3))) + (h.v * ld3(nn + 6)));
+        } else {
+            nl = normalize(cross(e1, e2));
+        }
+        pl = (v0 + (h.u * e1)) + (h.v * e2);
+    } else {                                                    // p = origin + dir * t, local ray
+        const V3 ol = m4_point(I.w2l, o - ld3(I.motion) * time, 1.0);
+        const V3 dl = m4_point(I.w2l, d, 0.0);
+        pl = ol + dl * h.t;
+        nl = (I.kind == kPrimSphere) ? normalize(pl - ld3(T.v0)) : normalize(ld3(T.e1));
+    }
+    p = m4_point(I.l2w, pl, 1.0) + ld3(I.motion) * time;
+    Ngeo = normalize(m3_mul(I.nmat, nl));
+    if (I.det_neg) Ngeo = -Ngeo;
 }
 
 // orthonormalBasis (Object+Extension.swift:531-552)

@@ -56,7 +56,17 @@ struct DInstance {        // Instance (RTContext.swift:43-61) + its BLAS entry p
     int32_t material;     // materialOverride (always set by makeInstance callers)
     int32_t smooth;       // prim shadingMode == .smooth
     int32_t det_neg;      // simd_determinant(M3) < 0
+    int32_t kind;         // BLAS primitive kind: kPrimTriangles / kPrimSphere / kPrimPlane
+    int32_t pad;
 };
+
+// Single-primitive BLASes of Sphere / Plane objects (RTContext.swift:122-192) keep their
+// primitive in one TriRec: sphere = {v0 = center, e1.x = radius}, plane = {v0 = center,
+// e1 = normal}.  Every sphere/plane is its own instance, so the kind lives in DInstance.
+constexpr int32_t kPrimTriangles = 0, kPrimSphere = 1, kPrimPlane = 2;
+
+struct DAreaLight { double position[3], normal[3], radiance[3], size; };   // ParsingKit AreaLight
+constexpr int kJitterCells = 100;    // buildStratifiedJitter 10x10 table (Object+Extension.swift:646-659)
 
 struct DTlasLeafEntry { int32_t inst; int32_t last; };
 
@@ -94,6 +104,12 @@ struct RenderParams {
     int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
     int32_t pad1;
+    const DAreaLight* alights;
+    const double* jitter;            // [0..99] jitterX, [100..199] jitterY
+    const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)
+    long long* events;               // k_events output: per-pixel area-light evaluations
+    int32_t num_alights;
+    int32_t has_special;             // spheres / planes present (general walk tests kinds)
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
     unsigned long long* counters;    // [0] shadow rays, [1] secondary rays, [2..8] work counters (kCounterWords)

@@ -49,23 +49,9 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         if (UNI) uni_closest<COUNT>(P, o, d, inv, tlo, h, st, c);
         else intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
         if (h.inst < 0) { L = ld3(P.background); break; }
-        // reconstruct the hit exactly as intersectTriangle + intersectTLAS wrote it
-        const TriRec& T = P.tris[h.tri];
+        V3 p, Ngeo;
+        hit_geometry<COUNT>(P, o, d, time, h, p, Ngeo, c);
         const DInstance& I = P.insts[h.inst];
-        const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
-        V3 nl;
-        if (I.smooth) {
-            if (COUNT) c.normals++;
-            const double* nn = P.normals + (size_t)h.tri * 9;
-            const double w = 1.0 - h.u - h.v;
-            nl = normalize(((w * ld3(nn)) + (h.u * ld3(nn + 3))) + (h.v * ld3(nn + 6)));
-        } else {
-            nl = normalize(cross(e1, e2));
-        }
-        const V3 pl = (v0 + (h.u * e1)) + (h.v * e2);
-        const V3 p = m4_point(I.l2w, pl, 1.0) + ld3(I.motion) * time;
-        V3 Ngeo = normalize(m3_mul(I.nmat, nl));
-        if (I.det_neg) Ngeo = -Ngeo;
         const int matIndex = max(0, min(P.num_mats - 1, I.material - 1));
         const DMaterial& M = P.mats[matIndex];
         const bool frontFacing = dot(d, Ngeo) < 0;
@@ -151,6 +137,11 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 #else
 #define MYRT_MEGA_ATTR
 #endif
+}  // namespace dev
+}  // namespace myrt
+#include "render_full.h"
+namespace myrt {
+namespace dev {
 // UNI: identity scenes walk TLAS + BLAS as one tree (device.h unified_step).
 template <bool COUNT, bool BOUNCE, bool UNI>
 __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams P) {
@@ -271,6 +262,11 @@ struct DeviceReplica {
     DTlasLeafEntry* tlas_leaf = nullptr;
     DMaterial* mats = nullptr;
     DPointLight* plights = nullptr;
+    DAreaLight* alights = nullptr;
+    double* jitter = nullptr;
+    long long* events = nullptr;              // area-light passes (grown on demand)
+    long long* jstart = nullptr;
+    int64_t cap_px = 0;
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -301,6 +297,7 @@ static void free_replica(DeviceReplica& r) {
     wave_release(r.wave);
     (void)hipFree(r.recs); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
+    (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -318,6 +315,8 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r) {
     if ((rc = upload(S.tlas_leaf, &r.tlas_leaf, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.mats, &r.mats, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.plights, &r.plights, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.alights, &r.alights, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.jitter, &r.jitter, r.bytes)) != RT_OK) return rc;
     HIP_TRY(hipMalloc((void**)&r.counters, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&r.ev0));
@@ -376,8 +375,6 @@ static DCamera camera_constants(const rt_camera& cam) {
 
 static int32_t check_renderable(const HostScene& S, int32_t cam) {
     if (cam < 0 || cam >= (int32_t)S.cams.size()) return fail(RT_ERR_INVALID_CAMERA, "Invalid camera index");
-    if (S.has_dielectric) return fail(RT_ERR_UNSUPPORTED, "dielectric materials are not implemented on the GPU path yet");
-    if (S.num_area_lights > 0) return fail(RT_ERR_UNSUPPORTED, "area lights are not implemented on the GPU path yet");
     if (S.max_depth > kMaxDepthGPU) return fail(RT_ERR_UNSUPPORTED, "maxRecursionDepth above the GPU limit");
     return RT_OK;
 }
@@ -422,6 +419,10 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
+    P.alights = r.alights;
+    P.jitter = r.jitter;
+    P.num_alights = (int32_t)S.alights.size();
+    P.has_special = S.has_special ? 1 : 0;
     return P;
 }
 
@@ -437,9 +438,38 @@ static bool use_megakernel() {
     return !(e && std::strcmp(e, "wave") == 0);
 }
 
+static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count) {
+    dim3 grid((unsigned)(((P.cam.width + 31) / 32) * P.num_chunks), 1, 1);
+    dim3 block(256, 1, 1);
+    const size_t lds = (size_t)dev::kLds * 256 * sizeof(unsigned long long);
+    if (P.num_alights > 0) {
+        const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
+        if (px > r.cap_px) {
+            (void)hipFree(r.events); (void)hipFree(r.jstart);
+            r.events = nullptr; r.jstart = nullptr; r.cap_px = 0;
+            if (hipMalloc((void**)&r.events, px * sizeof(long long)) != hipSuccess ||
+                hipMalloc((void**)&r.jstart, px * sizeof(long long)) != hipSuccess)
+                return fail(RT_ERR_OOM, "device allocation of area-light jitter buffers failed");
+            r.cap_px = px;
+        }
+        P.events = r.events;
+        P.jstart = r.jstart;
+        hipLaunchKernelGGL(dev::k_events, grid, block, lds, stream, P);
+        hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), block, 0, stream, P);
+    }
+    if (count) hipLaunchKernelGGL((dev::render_full<true>), grid, block, lds, stream, P);
+    else hipLaunchKernelGGL((dev::render_full<false>), grid, block, lds, stream, P);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
 static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {
     if (P.num_chunks == 0) return RT_OK;
-    if (!use_megakernel() && !P.count_ref) {   // reference-order counting is a megakernel mode
+    // dielectrics and area lights: the full trace() (render_full.h); it and spheres/planes
+    // exist only as megakernels
+    const bool full = s->host.has_dielectric || P.num_alights > 0;
+    if (full) return launch_full(r, P, stream, count);
+    if (!use_megakernel() && !P.count_ref && !P.has_special) {   // ref-order counting is a megakernel mode
         const bool bounce_w = scene_has_bounce(s->host) && P.max_depth > 0;
         const int32_t rc = wave_render(P, r.wave, bounce_w, count, stream);
         if (rc != RT_OK) return fail(rc, rc == RT_ERR_OOM ? "device allocation of wavefront queues failed"

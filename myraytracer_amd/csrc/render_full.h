@@ -1,0 +1,379 @@
+// render_full.h — the complete trace() for scenes the fast megakernel does not take:
+// dielectric materials (two child rays per bounce) and area lights (the chunk-sequential
+// jitterIndex).  Included by render.hip.
+//
+// trace() (Object+Extension.swift:96-283) recurses depth-first: reflection subtree, then
+// transmission subtree.  Here the recursion is an explicit per-lane frame stack (private
+// memory, <= maxRecursionDepth + 1 frames) visited in the same order, so the PCG32 draws
+// (roughness, :193-198, :209-216, :258-263) and the area-light jitterIndex increments
+// (:152-154) happen in the reference's sequence.
+//
+// jitterIndex is one counter per 8-row chunk that runs through the chunk's pixels in
+// row-major order (:288, Renderer.renderChunk).  A lane cannot know how many area-light
+// evaluations the pixels before it made, so area-light frames take three launches:
+//   k_events   - the same paths without lighting, counting evaluations per pixel
+//                (an evaluation = one area light at one hit with computeDirectLight);
+//   k_jscan    - per-chunk exclusive prefix sum in row-major pixel order;
+//   render_full- the real render, each pixel starting at its prefix.
+#pragma once
+
+namespace myrt {
+namespace dev {
+
+enum : int { kFrameMirror = 1, kFrameDielR = 2, kFrameDielT = 3 };
+
+struct Frame {            // one suspended trace() level waiting for a child
+    V3 Lo;                // radiance of this level so far
+    V3 p;                 // hit point (transmission origin)
+    V3 aux;               // mirror/conductor: multiplier; dielectric: LiR once known
+    V3 td;                // dielectric: transmitted direction
+    double R;             // dielectric: Fresnel reflectance
+    double t;             // this level's hit distance (its parent's Beer test)
+    int hitmat;           // hit.mat (materialOverride) of this level
+    int mat;              // clamped material index
+    int state;
+    bool tir, entering;
+};
+
+struct LevelOut { V3 L; bool hit; int hitmat; double t; };
+
+// fresnelDielectric (Object+Extension.swift:467-491)
+__device__ __forceinline__ void fresnel_dielectric(double n1, double n2, double cosI, double& R, bool& hasCosT,
+                                                   double& cosT, double& sin2T) {
+    const double cosTheta = smax(0.0, smin(1.0, fabs(cosI)));
+    const double eta = n1 / n2;
+    sin2T = (eta * eta) * smax(0.0, 1.0 - cosTheta * cosTheta);
+    if (sin2T > 1.0) { R = 1.0; hasCosT = false; cosT = 0; return; }
+    const double cosPhi = dsqrt(smax(0.0, 1.0 - sin2T));
+    const double Rs = (n2 * cosTheta - n1 * cosPhi) / (n2 * cosTheta + n1 * cosPhi);
+    const double Rp = (n1 * cosTheta - n2 * cosPhi) / (n1 * cosTheta + n2 * cosPhi);
+    R = 0.5 * (Rs * Rs + Rp * Rp);
+    hasCosT = true;
+    cosT = cosPhi;
+}
+
+// EVENTS: count area-light evaluations only (no light sampling, no shadow rays); the
+// paths, PCG32 draws and jitterIndex increments are the same as the real render.
+template <bool COUNT, bool EVENTS>
+__device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng,
+                         long long& jitterIndex, Stack& st, Counts& c) {
+    Frame F[kMaxDepthGPU + 1];
+    int depth = 0;
+    LevelOut out;
+    for (;;) {
+        // ======================================================== enter level `depth`
+        bool descend = false;
+        if (depth > P.max_depth) {                                   // :97
+            out = LevelOut{ld3(P.background), false, 0, DINF};
+        } else if (!P.has_tlas) {                                    // :98
+            out = LevelOut{v3(0, 0, 0), false, 0, DINF};
+        } else {
+            Hit h;
+            intersect_closest<COUNT>(P, o, d, rcp(d), tlo, time, h, st, c);
+            if (h.inst < 0) {                                        // :101-103
+                out = LevelOut{ld3(P.background), false, 0, DINF};
+            } else {
+                V3 p, Ngeo;
+                hit_geometry<COUNT>(P, o, d, time, h, p, Ngeo, c);
+                const int hitmat = P.insts[h.inst].material;
+                const int mi = max(0, min(P.num_mats - 1, hitmat - 1));
+                const DMaterial& M = P.mats[mi];
+                const bool frontFacing = dot(d, Ngeo) < 0;
+                const V3 N = frontFacing ? Ngeo : -Ngeo;
+                const bool computeDirect = !(M.ior > 0) || frontFacing;
+                V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+                if (computeDirect) {
+                    if (!EVENTS) {
+                        for (int li = 0; li < P.num_plights; ++li) {        // :118-143
+                            const DPointLight& PL = P.plights[li];
+                            V3 wi = ld3(PL.position) - p;
+                            const double dist = length(wi);
+                            wi = normalize(wi);
+                            c.shadow++;
+                            const double NdotL = smax(0.0, dot(N, wi));
+                            if (NdotL > 0 || MYRT_REF(P)) {                 // else the result is discarded
+                                const bool blocked = occluded<COUNT>(P, p + wi * P.shadow_eps, wi, dist, time, st, c);
+                                if (!blocked && NdotL > 0) {
+                                    const double shininess = smax(1.0, M.phong);
+                                    const V3 Ld = ld3(M.diffuse) * NdotL;
+                                    const V3 view = normalize(-d);
+                                    const V3 hv = normalize(wi + view);
+                                    const double NdotH = smax(0.0, dot(N, hv));
+                                    const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
+                                    const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
+                                    Lo = Lo + (Ld + Ls) * atten;
+                                }
+                            }
+                        }
+                    }
+                    for (int ai = 0; ai < P.num_alights; ++ai) {            // :145-186
+                        if (EVENTS) { jitterIndex += 1; continue; }
+                        const DAreaLight& AL = P.alights[ai];
+                        const V3 nL = normalize(ld3(AL.normal));
+                        V3 tg, bt;
+                        onb(nL, tg, bt);
+                        const double size = AL.size;
+                        const double area = size * size;
+                        const int cell = (int)(jitterIndex % kJitterCells);
+                        const double r1 = P.jitter[cell] / 10.0 - 0.5;
+                        const double r2 = P.jitter[kJitterCells + cell] / 10.0 - 0.5;
+                        jitterIndex += 1;
+                        const V3 samplePos = (ld3(AL.position) + tg * (r1 * size)) + bt * (r2 * size);
+                        V3 wi = samplePos - p;
+                        const double dist2 = dot(wi, wi);
+                        const double dist = dsqrt(dist2);
+                        wi = wi / dist;
+                        const double NdotL = dot(N, wi);
+                        if (NdotL <= 0) continue;
+                        const double Ln = fabs(dot(nL, -wi));
+                        if (Ln <= 0) continue;
+                        c.shadow++;
+                        if (occluded<COUNT>(P, p + wi * P.shadow_eps, wi, dist - P.shadow_eps, time, st, c)) continue;
+                        const V3 view = normalize(-d);
+                        const V3 hv = normalize(wi + view);
+                        const V3 Ld = ld3(M.diffuse) * NdotL;
+                        const V3 Ls = ld3(M.specular) * pow(smax(0.0, dot(N, hv)), M.phong);
+                        const V3 brdf = Ld + Ls;
+                        const V3 contrib = ((brdf * ld3(AL.radiance)) * (Ln / dist2)) * area;
+                        Lo = Lo + contrib;
+                    }
+                }
+                Frame& f = F[depth];
+                f.Lo = Lo; f.p = p; f.t = h.t; f.hitmat = hitmat; f.mat = mi;
+                if ((M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && depth < P.max_depth) {   // :189-206, :252-275
+                    if (M.type == RT_MAT_MIRROR) {
+                        f.aux = ld3(M.mirror);
+                    } else {
+                        const double cosI = smax(0.0, -dot(d, N));
+                        f.aux = fresnel_conductor(M.ior, M.absorption_index, cosI) * ld3(M.mirror);
+                    }
+                    V3 rd = normalize(reflect(d, N));
+                    if (M.roughness != 0.0) {
+                        V3 tg, bt;
+                        onb(rd, tg, bt);
+                        const double rand1 = rng.nextFloat() - 0.5;
+                        const double rand2 = rng.nextFloat() - 0.5;
+                        rd = (rd + (M.roughness * rand1) * bt) + (M.roughness * rand2) * tg;
+                        rd = normalize(rd);
+                    }
+                    f.state = kFrameMirror;
+                    c.secondary++;
+                    o = p + N * P.shadow_eps;
+                    d = rd;
+                    tlo = 0.0;
+                    descend = true;
+                } else if (M.type == RT_MAT_DIELECTRIC && depth < P.max_depth) {                    // :207-251
+                    V3 mfN = N;
+                    if (M.roughness != 0.0) {
+                        V3 tg, bt;
+                        onb(N, tg, bt);
+                        const double r1 = (rng.nextFloat() * 2.0) - 1.0;
+                        const double r2 = (rng.nextFloat() * 2.0) - 1.0;
+                        mfN = normalize((N + ((tg * r1) * M.roughness)) + ((bt * r2) * M.roughness));
+                    }
+                    const bool entering = frontFacing;
+                    const double n1 = entering ? 1.0 : M.ior;
+                    const double n2 = entering ? M.ior : 1.0;
+                    const double cosI = -dot(d, mfN);
+                    double R, cosT, sin2T;
+                    bool hasCosT;
+                    fresnel_dielectric(n1, n2, cosI, R, hasCosT, cosT, sin2T);
+                    const V3 rd = normalize(reflect(d, mfN));
+                    f.tir = !hasCosT || sin2T > 1;
+                    if (!f.tir) {
+                        const double eta = n1 / n2;
+                        f.td = normalize((d * eta) + (mfN * (eta * cosI - cosT)));
+                    }
+                    f.R = R;
+                    f.entering = entering;
+                    f.state = kFrameDielR;
+                    c.secondary++;
+                    o = p + rd * P.shadow_eps;
+                    d = rd;
+                    tlo = 0.0;
+                    descend = true;
+                } else {
+                    out = LevelOut{isfin(Lo) ? Lo : v3(0, 0, 0), true, hitmat, h.t};   // :277-280
+                }
+            }
+        }
+        if (descend) { depth++; continue; }
+        // ======================================================== return to parents
+        for (;;) {
+            if (depth == 0) return out.L;
+            depth--;
+            Frame& f = F[depth];
+            if (f.state == kFrameMirror) {
+                const V3 Lo = f.Lo + f.aux * out.L;
+                out = LevelOut{isfin(Lo) ? Lo : v3(0, 0, 0), true, f.hitmat, f.t};
+                continue;
+            }
+            if (f.state == kFrameDielR) {
+                if (f.tir) {
+                    const V3 Lo = f.Lo + out.L;
+                    out = LevelOut{isfin(Lo) ? Lo : v3(0, 0, 0), true, f.hitmat, f.t};
+                    continue;
+                }
+                f.aux = out.L;                                       // LiR
+                f.state = kFrameDielT;
+                c.secondary++;
+                o = f.p + f.td * P.shadow_eps;                       // Ray(origin:dir:time:), tMin 0
+                d = f.td;
+                tlo = 0.0;
+                depth++;
+                descend = true;
+                break;
+            }
+            // kFrameDielT
+            V3 LiT = out.L;
+            const DMaterial& M = P.mats[f.mat];
+            const bool absNonZero = !(M.absorption[0] == 0 && M.absorption[1] == 0 && M.absorption[2] == 0);
+            if (f.entering && absNonZero && out.hit && out.hitmat == f.hitmat) {   // beerAttenuate quirk
+                const double dd = smax(out.t, 0.0);
+                const V3 a = -ld3(M.absorption) * dd;
+                const V3 att = (__builtin_isfinite(dd) && dd > 0) ? v3(exp(a.x), exp(a.y), exp(a.z)) : LiT;
+                LiT = LiT * att;
+            }
+            const V3 Lo = f.Lo + ((f.aux * f.R) + (LiT * (1.0 - f.R)));
+            out = LevelOut{isfin(Lo) ? Lo : v3(0, 0, 0), true, f.hitmat, f.t};
+        }
+        if (!descend) return out.L;
+    }
+}
+
+// Pixel loop shared by k_events and render_full (Object+Extension.swift:292-356).
+template <bool COUNT, bool EVENTS>
+__device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, long long& jitterIndex, Stack& st,
+                                         Counts& c) {
+    const DCamera& C = P.cam;
+    PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
+    V3 pixel = v3(0, 0, 0);
+    const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
+    const int n = C.n;
+    int sampleIndex = 0;
+    for (int sy = 0; sy < n && sampleIndex < C.samples; ++sy) {
+        for (int sx = 0; sx < n; ++sx) {
+            const double xi1 = rng.nextFloat();
+            const double xi2 = rng.nextFloat();
+            const double currentI = (double)i + ((double)sx + xi1) / (double)n;
+            const double currentJ = (double)j + ((double)sy + xi2) / (double)n;
+            const V3 s = (q00 - v * (currentJ * C.dv)) + u * (currentI * C.du);
+            const V3 dir0 = normalize(s - eye);
+            V3 dir = dir0, camEye = eye;
+            if (C.aperture > 0 && C.focus > 0) {                      // :325-338
+                const V3 forward = -w;
+                const double denom = dot(dir0, forward);
+                const double tFocus = fabs(denom) < 1e-6 ? C.focus : (C.focus / denom);
+                const V3 pFocus = eye + dir0 * tFocus;
+                const double uRand = rng.nextFloat() - 0.5;
+                const double vRand = rng.nextFloat() - 0.5;
+                const V3 lensOffset = ((uRand * u) + (vRand * v)) * C.aperture;
+                const V3 a = eye + lensOffset;
+                dir = normalize(pFocus - a);
+                camEye = a;
+            }
+            const double time = rng.nextFloat();
+            const double denom = dot(dir, w);
+            const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
+            pixel = pixel + trace_full<COUNT, EVENTS>(P, camEye, dir, smax(tImg, 0.0), time, rng, jitterIndex, st, c);
+            sampleIndex += 1;
+            if (sampleIndex >= C.samples) break;
+        }
+    }
+    return pixel;
+}
+
+__device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int& j, int& slot, int& row) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int gx = (P.cam.width + 31) >> 5;
+    const int tile = (int)blockIdx.x;
+    i = (tile % gx) * 32 + wave * 8 + (lane & 7);
+    slot = tile / gx;
+    const int chunk = P.chunk_first + slot * P.chunk_step;
+    row = lane >> 3;
+    j = chunk * 8 + row;
+}
+
+// Pass 1: area-light evaluations per pixel of the selection (packed rows).
+__global__ __launch_bounds__(256) void k_events(RenderParams P) {
+    extern __shared__ unsigned long long lds_stack[];
+    int i, j, slot, row;
+    full_pixel_of(P, i, j, slot, row);
+    if (i >= P.cam.width || j >= P.cam.height) return;
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    MYRT_STACK(st, lds_stack);
+    long long events = 0;
+    (void)pixel_full<false, true>(P, i, j, events, st, cnt);
+    P.events[((size_t)slot * 8 + row) * (size_t)P.cam.width + i] = events;
+}
+
+// Pass 2: exclusive prefix of the events over each chunk, row-major (one block per chunk).
+__global__ __launch_bounds__(256) void k_jscan(RenderParams P) {
+    __shared__ long long part[256];
+    const int slot = blockIdx.x;
+    const int chunk = P.chunk_first + slot * P.chunk_step;
+    const int rows = min(8, P.cam.height - chunk * 8);
+    const long long n = (long long)rows * P.cam.width;
+    const size_t base = (size_t)slot * 8 * (size_t)P.cam.width;
+    const long long seg = (n + 255) / 256;
+    const long long b = min(n, (long long)threadIdx.x * seg), e = min(n, b + seg);
+    long long sum = 0;
+    for (long long k = b; k < e; ++k) sum += P.events[base + k];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long run = 0;
+        for (int t = 0; t < 256; ++t) { const long long x = part[t]; part[t] = run; run += x; }
+    }
+    __syncthreads();
+    long long run = part[threadIdx.x];
+    long long* js = const_cast<long long*>(P.jstart);
+    for (long long k = b; k < e; ++k) { js[base + k] = run; run += P.events[base + k]; }
+}
+
+// Pass 3 (or the only pass without area lights): the render.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void render_full(RenderParams P) {
+    extern __shared__ unsigned long long lds_stack[];
+    int i, j, slot, row;
+    full_pixel_of(P, i, j, slot, row);
+    const bool valid = (i < P.cam.width) && (j < P.cam.height);
+    const int lane = threadIdx.x & 63;
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    if (valid) {
+        MYRT_STACK(st, lds_stack);
+        const size_t o = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
+        long long jitterIndex = P.num_alights > 0 ? P.jstart[o] : 0;
+        const V3 px = pixel_full<COUNT, false>(P, i, j, jitterIndex, st, cnt) / (double)P.cam.samples;
+        if (P.out_rgb) {
+            P.out_rgb[o * 3 + 0] = px.x;
+            P.out_rgb[o * 3 + 1] = px.y;
+            P.out_rgb[o * 3 + 2] = px.z;
+        }
+        if (P.out_rgba8) {                                           // RayTracer.swift:186-195
+            const double cx = fmin(fmax(px.x, 0.0), 255.0), cy = fmin(fmax(px.y, 0.0), 255.0),
+                         cz = fmin(fmax(px.z, 0.0), 255.0);
+            const unsigned packed = (unsigned)(unsigned char)cx | ((unsigned)(unsigned char)cy << 8) |
+                                    ((unsigned)(unsigned char)cz << 16) | (255u << 24);
+            reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
+        }
+    }
+    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary);
+    if (lane == 0) {
+        if (s0) atomicAdd(&P.counters[0], s0);
+        if (s1) atomicAdd(&P.counters[1], s1);
+    }
+    if (COUNT) {
+        const unsigned long long a = wave_sum(cnt.recs), b = wave_sum(cnt.tris), cc = wave_sum(cnt.normals),
+                                 dd = wave_sum(cnt.insts), ee = wave_sum(valid ? 1ull : 0ull);
+        if (lane == 0) {
+            atomicAdd(&P.counters[2], a); atomicAdd(&P.counters[3], b); atomicAdd(&P.counters[4], cc);
+            atomicAdd(&P.counters[5], dd); atomicAdd(&P.counters[6], ee);
+        }
+        const unsigned long long ff = wave_sum(cnt.nodes), gg = wave_sum(cnt.smooth);
+        if (lane == 0 && P.count_ref) { atomicAdd(&P.counters[7], ff); atomicAdd(&P.counters[8], gg); }
+    }
+}
+
+}  // namespace dev
+}  // namespace myrt

@@ -23,6 +23,8 @@ static inline D3 d3(double x, double y, double z) { return D3{x, y, z}; }
 static inline D3 operator+(D3 a, D3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
 static inline D3 operator-(D3 a, D3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 static inline D3 operator*(D3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+static inline D3 operator-(D3 a, double s) { return {a.x - s, a.y - s, a.z - s}; }
+static inline D3 operator+(D3 a, double s) { return {a.x + s, a.y + s, a.z + s}; }
 static inline D3 operator*(double s, D3 a) { return {s * a.x, s * a.y, s * a.z}; }
 static inline D3 operator/(D3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
 static inline double dot(D3 a, D3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
@@ -276,6 +278,8 @@ struct BlasBuild {
     PrimSet prims;
     RefBVH bvh;
     bool smooth = false;
+    int32_t kind = kPrimTriangles;   // kPrimSphere / kPrimPlane: one primitive, bounds pmin/pmax
+    D3 pmin{0, 0, 0}, pmax{0, 0, 0};
     D3 motion{0, 0, 0};
     uint64_t hash = 0;
     int64_t depth = 0;
@@ -367,6 +371,36 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         S.plights.push_back(l);
     }
     S.num_area_lights = d->num_area_lights;
+    for (int i = 0; i < d->num_area_lights; ++i) {
+        const rt_area_light& a = d->area_lights[i];
+        DAreaLight l{};
+        l.position[0] = a.position.x; l.position[1] = a.position.y; l.position[2] = a.position.z;
+        l.normal[0] = a.normal.x; l.normal[1] = a.normal.y; l.normal[2] = a.normal.z;
+        l.radiance[0] = a.radiance.x; l.radiance[1] = a.radiance.y; l.radiance[2] = a.radiance.z;
+        l.size = a.size;
+        S.alights.push_back(l);
+    }
+    {   // buildStratifiedJitter (Object+Extension.swift:92-93, 646-659): PCG32(0x123456789ABCDEF),
+        // cell (gx, gy) row-major, x draw then y draw
+        uint64_t state = 0, inc = (0x123456789ABCDEFull << 1) | 1u;
+        auto next = [&]() -> uint32_t {
+            const uint64_t old = state;
+            state = old * 6364136223846793005ull + inc;
+            const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+            const uint32_t rot = (uint32_t)(old >> 59);
+            return (xs >> rot) | (xs << ((~rot + 1u) & 31u));
+        };
+        next();
+        state += 0x9E3779B97F4A7C15ull;
+        next();
+        S.jitter.assign(2 * kJitterCells, 0.0);
+        int q = 0;
+        for (int gy = 0; gy < 10; ++gy)
+            for (int gx = 0; gx < 10; ++gx, ++q) {
+                S.jitter[q] = (double)gx + (double)next() * 2.3283064365386963e-10;
+                S.jitter[kJitterCells + q] = (double)gy + (double)next() * 2.3283064365386963e-10;
+            }
+    }
     for (int i = 0; i < d->num_cameras; ++i) S.cams.push_back(d->cameras[i]);
 
     // ---- flatten objects (RTContext.swift:120-378)
@@ -399,8 +433,39 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
 
     for (int oi = 0; oi < d->num_objects; ++oi) {
         const rt_object& o = d->objects[oi];
-        if (o.kind == RT_OBJ_SPHERE) { err = "spheres are not implemented on the GPU path yet"; S.n_spheres++; return RT_ERR_UNSUPPORTED; }
-        if (o.kind == RT_OBJ_PLANE) { err = "planes are not implemented on the GPU path yet"; S.n_planes++; return RT_ERR_UNSUPPORTED; }
+        if (o.kind == RT_OBJ_SPHERE || o.kind == RT_OBJ_PLANE) {            // RTContext.swift:122-192
+            const bool sph = o.kind == RT_OBJ_SPHERE;
+            (sph ? S.n_spheres : S.n_planes)++;
+            S.has_special = true;
+            Tri t{};
+            t.v0 = of(o.center);
+            t.e1 = sph ? d3(o.radius, 0, 0) : of(o.normal);
+            const int64_t gi = (int64_t)triangles.size();
+            triangles.push_back(t);
+            BlasBuild bb;
+            bb.kind = sph ? kPrimSphere : kPrimPlane;
+            bb.smooth = true;                                                // shadingMode .smooth (unused)
+            bb.triIndex.push_back(gi);
+            bb.prims.n = 1;
+            if (sph) {                                                       // center -/+ radius
+                bb.pmin = t.v0 - o.radius;
+                bb.pmax = t.v0 + o.radius;
+            } else {                                                         // +-1e5 box, centroid 0
+                bb.pmin = d3(-1e5, -1e5, -1e5);
+                bb.pmax = d3(1e5, 1e5, 1e5);
+            }
+            const D3 c = sph ? t.v0 : d3(0, 0, 0);
+            bb.prims.bmin = {bb.pmin.x, bb.pmin.y, bb.pmin.z};
+            bb.prims.bmax = {bb.pmax.x, bb.pmax.y, bb.pmax.z};
+            bb.prims.cen = {c.x, c.y, c.z};
+            blases.push_back(std::move(bb));
+            InstBuild ib{};
+            ib.blas = (int)blases.size() - 1;
+            std::memcpy(ib.M, o.transform, sizeof(ib.M));
+            ib.material = o.material_id; ib.motion = d3(0, 0, 0);
+            insts.push_back(ib);
+            continue;
+        }
         if (o.kind == RT_OBJ_TRIANGLE) {                                      // RTContext.swift:193-235
             S.n_tris++;
             blases.push_back(singleTriBlas(o));
@@ -570,7 +635,13 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         const BlasBuild& bb = blases[ib.blas];
         // world bounds: union of every prim's transformed bounds
         D3 mn = d3(kInf, kInf, kInf), mx = d3(-kInf, -kInf, -kInf);
-        for (size_t q = 0; q < bb.triIndex.size(); ++q) {
+        if (bb.kind != kPrimTriangles) {
+            double lo[3] = {bb.pmin.x, bb.pmin.y, bb.pmin.z}, hi[3] = {bb.pmax.x, bb.pmax.y, bb.pmax.z}, olo[3], ohi[3];
+            aabb_transformed(lo, hi, ib.M, olo, ohi);
+            mn = d3(olo[0], olo[1], olo[2]);
+            mx = d3(ohi[0], ohi[1], ohi[2]);
+        }
+        for (size_t q = 0; q < bb.triIndex.size() && bb.kind == kPrimTriangles; ++q) {
             const Tri& t = triangles[bb.triIndex[q]];
             D3 pmn = vmin(t.v0, vmin(t.v1, t.v2)), pmx = vmax(t.v0, vmax(t.v1, t.v2));
             if (!(bb.motion.x == 0 && bb.motion.y == 0 && bb.motion.z == 0)) {
@@ -602,6 +673,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         di.material = ib.material;
         di.smooth = bb.smooth ? 1 : 0;
         di.det_neg = m3_det_of4(ib.M) < 0.0 ? 1 : 0;
+        di.kind = bb.kind;
         S.insts.push_back(di);
         S.inst_bvh_hash.push_back(bb.hash);
     }
@@ -644,6 +716,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             owners[ib.blas]++;
         }
         for (int o : owners) ident &= (o <= 1);
+        ident &= !S.has_special;                    // the unified walk tests triangles only
         S.identity = ident;
         if (ident) {
             for (size_t i = 0; i < insts.size(); ++i) {

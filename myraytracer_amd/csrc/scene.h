@@ -45,7 +45,10 @@ struct HostScene {
     int32_t max_depth = 0;
     std::vector<DMaterial> mats;
     std::vector<DPointLight> plights;
+    std::vector<DAreaLight> alights;
+    std::vector<double> jitter;            // 2 x kJitterCells (buildStratifiedJitter)
     int32_t num_area_lights = 0;
+    bool has_special = false;              // sphere / plane objects present
     std::vector<rt_camera> cams;
     bool has_dielectric = false;
     // ---- device layout (host copies)
