@@ -105,6 +105,7 @@ def main():
     n = int(max(1, cam.num_samples) ** 0.5)
     rays_primary = rows * W * n * n
     rays_shadow = int(st.shadow_rays)
+    rays_secondary = int(st.secondary_rays)     # reflection rays: reported, not in `value`
     rays_rank = rays_primary + rays_shadow
 
     # ---- timed region: K frames, barrier + sync on both sides
@@ -182,7 +183,8 @@ def main():
             "dtype": "f64", "data": "synthetic (seeded scene generator; no bunny/assets offline)",
             "config": {"workload": workload, "width": W, "height": H, "spp": max(1, cam.num_samples),
                        "triangles": int(info.triangles), "partition": f"8-row chunks round-robin over {world} GPU(s)",
-                       "rays_per_frame": int(rays_rank) if world == 1 else None},
+                       "rays_per_frame": int(rays_rank) if world == 1 else None,
+                       "secondary_rays_per_frame": rays_secondary if world == 1 else None},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
