@@ -7,17 +7,20 @@ Workload (BASELINE.json configs[2], "C3"): a ~1.02M-triangle single-mesh PLY sce
 hot path (primary ray generation, TLAS/BLAS traversal, Moeller-Trumbore, Whitted
 shading with shadow rays), FP64, scene and output resident in HBM.
 
-N GPUs (torchrun, one process per GPU): configs[3] "C4" — the SAME frame tile-
-partitioned: 8-row chunk c goes to rank c mod N (no collective on the data path; the
-framebuffer stays distributed in HBM).  Total work is fixed -> "scaling": "strong".
+N GPUs (torchrun, one process per GPU): pixels are independent (each seeds its own
+PCG32), so the path shards with no collective on the data path.  Default
+`--scaling weak` (the contract for a partitioned path): every rank renders one full C3
+frame per step from its own scene replica - per-GPU work is fixed as N grows.
+`--scaling strong` is configs[3] "C4": ONE frame, 8-row chunk c on rank c mod N.
 
 Timed region: K frames bracketed by barrier + device sync; value = (primary + shadow
-rays of all ranks) / max-over-ranks wall time.  The roofline object prices the render
-kernel: algorithmic bytes (128 B per two-child node record fetched, 80 B per triangle
-tested, 72 B per smooth-normal fetch, 24 B per pixel written; counted by an
-instrumented variant of the same kernel) / average kernel duration from HIP events on
-the launch stream.  cpu_baseline: the C++ restatement of the reference CPU renderer
-(oracle/, test infrastructure) on a bounded sample of the same frame, rank 0, N = 1.
+rays of all ranks) / max-over-ranks wall time.  Roofline: algorithmic
+bytes B = 56 N_nodeFetch + 72 N_triTest + 72 N_smoothHit + 24 N_pixel counted in the
+reference's traversal order by a counting launch (equal to the oracle's tally), divided
+by the average frame time from HIP events on the launch stream; `traffic` = PMC HBM
+bytes per launch from profiles/traffic_<config>.json (tools/pmc_traffic.py).
+cpu_baseline: the C++ restatement of the reference CPU renderer (oracle/, test
+infrastructure) on a bounded sample of the same frame, rank 0, N = 1.
 """
 from __future__ import annotations
 
@@ -39,7 +42,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
-    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+    p.add_argument("--scaling", default="weak", choices=["strong", "weak"],
                    help="strong: one frame tile-partitioned over ranks (C4); weak: every rank renders a full frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
@@ -64,6 +67,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
+    # MYRT_BENCH_DEVICE pins every rank to one device: rehearsing N ranks on a 1-GPU box
+    dev_override = os.environ.get("MYRT_BENCH_DEVICE")
+    local = int(dev_override) if dev_override is not None else local
     torch.cuda.set_device(local)
 
     import myraytracer_amd as M
@@ -182,7 +188,9 @@ def main():
             "scaling": "strong" if args.scaling == "strong" else "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (seeded scene generator; no bunny/assets offline)",
             "config": {"workload": workload, "width": W, "height": H, "spp": max(1, cam.num_samples),
-                       "triangles": int(info.triangles), "partition": f"8-row chunks round-robin over {world} GPU(s)",
+                       "triangles": int(info.triangles),
+                       "partition": (f"8-row chunks round-robin over {world} GPU(s)" if args.scaling == "strong"
+                                     else f"one full frame per GPU per step, {world} GPU(s), no collective"),
                        "rays_per_frame": int(rays_rank) if world == 1 else None,
                        "secondary_rays_per_frame": rays_secondary if world == 1 else None},
             "roofline": roofline,

@@ -228,7 +228,10 @@ def _ply_or_inline(path_dir, name, pos, faces, smooth, mid, mat, inline):
     os.makedirs(path_dir, exist_ok=True)
     path = os.path.join(path_dir, name)
     if not os.path.exists(path):
-        write_ply(path, pos, faces)
+        # several ranks may generate the same scene at once: write privately, publish atomically
+        tmp = f"{path}.{os.getpid()}.tmp"
+        write_ply(tmp, pos, faces)
+        os.replace(tmp, path)
     return Mesh(id=mid, material=mat, ply_path=path, shading_mode=smooth)
 
 
