@@ -316,7 +316,7 @@ struct Parser {
         const bool big = fileType == 2;
         for (auto& p : e.props) {
             if (p.countType == T_NONE) { p.raw.reserve((size_t)e.count * kSize[p.type]); }
-            else { p.counts.reserve(e.count); }
+            else { p.counts.reserve(e.count); p.listRaw.reserve((size_t)e.count * 3 * kSize[p.type]); }
         }
         if (fileType == 0) {
             const char* s = buf.data() + pos;
@@ -350,30 +350,35 @@ struct Parser {
             pos = (size_t)(s - buf.data());
             return true;
         }
+        // binary: values are copied straight into each property's column (no per-byte
+        // container appends); byte order is fixed up in place
         const size_t avail = buf.size() - 1;
+        for (auto& p : e.props)
+            if (p.countType == T_NONE) p.raw.resize((size_t)e.count * kSize[p.type]);
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(buf.data());
         for (int64_t r = 0; r < e.count; ++r) {
             for (auto& p : e.props) {
                 if (p.countType == T_NONE) {
                     const int n = kSize[p.type];
                     if (pos + n > avail) { err = "truncated binary PLY"; return false; }
-                    uint8_t v[8]; std::memcpy(v, buf.data() + pos, n); pos += n;
+                    uint8_t* v = p.raw.data() + (size_t)r * n;
+                    std::memcpy(v, src + pos, n); pos += n;
                     if (big) swap_bytes(v, n);
-                    p.raw.insert(p.raw.end(), v, v + n);
                 } else {
                     const int cn = kSize[p.countType];
                     if (pos + cn > avail) { err = "truncated binary PLY"; return false; }
-                    uint8_t c[8]; std::memcpy(c, buf.data() + pos, cn); pos += cn;
+                    uint8_t c[8]; std::memcpy(c, src + pos, cn); pos += cn;
                     if (big) swap_bytes(c, cn);
                     const int32_t cnt = raw_to_int(c, p.countType);
                     if (cnt < 0) { err = "negative list count"; return false; }
                     p.counts.push_back((uint32_t)cnt);
                     const int n = kSize[p.type];
-                    if (pos + (size_t)n * cnt > avail) { err = "truncated binary PLY"; return false; }
-                    for (int k = 0; k < cnt; ++k) {
-                        uint8_t v[8]; std::memcpy(v, buf.data() + pos, n); pos += n;
-                        if (big) swap_bytes(v, n);
-                        p.listRaw.insert(p.listRaw.end(), v, v + n);
-                    }
+                    const size_t bytes = (size_t)n * cnt;
+                    if (pos + bytes > avail) { err = "truncated binary PLY"; return false; }
+                    const size_t at = p.listRaw.size();
+                    p.listRaw.resize(at + bytes);
+                    std::memcpy(p.listRaw.data() + at, src + pos, bytes); pos += bytes;
+                    if (big) for (int k = 0; k < cnt; ++k) swap_bytes(p.listRaw.data() + at + (size_t)k * n, n);
                 }
             }
         }

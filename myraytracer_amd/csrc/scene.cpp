@@ -8,7 +8,11 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <atomic>
 #include <limits>
 #include <map>
 #include <memory>
@@ -39,6 +43,27 @@ static inline double smax(double x, double y) { return (y >= x) ? y : x; }  // S
 // ------------------------------------------------------- reference-exact BVH build
 // BVHBuilder.init/subdivide/findBestSplitPlane (BVH.swift:78-250).
 namespace {
+int build_threads() {                  // MYRT_BUILD_THREADS, default: hardware threads (<= 64)
+    static const int n = [] {
+        const char* e = std::getenv("MYRT_BUILD_THREADS");
+        const int v = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(v, 64));
+    }();
+    return n;
+}
+constexpr int64_t kParallelFold = 1 << 19;   // nodes this large fold their prims on several threads
+int par_chunks(int64_t count) {
+    if (count < kParallelFold) return 1;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(build_threads(), count / (kParallelFold / 8)));
+}
+template <class F>
+void run_chunks(int T, F&& f) {
+    if (T <= 1) { f(0); return; }
+    std::vector<std::thread> th;
+    for (int k = 1; k < T; ++k) th.emplace_back([&f, k] { f(k); });
+    f(0);
+    for (auto& t : th) t.join();
+}
 struct Builder {
     const PrimSet& P;
     RefBVH& B;
@@ -50,14 +75,24 @@ struct Builder {
     Builder(const PrimSet& p, RefBVH& b, int ml, int bins) : P(p), B(b), maxLeaf(ml), N(std::max(2, bins)) {
         binLo.resize(3 * N * 3); binHi.resize(3 * N * 3); binCnt.resize(3 * N);
     }
-    void updateNodeBounds(int64_t idx) {                                  // :108-124
-        D3 mn = d3(kInf, kInf, kInf), mx = d3(-kInf, -kInf, -kInf);
+    // updateNodeBounds (:108-124).  Large nodes fold chunks concurrently and merge the
+    // chunk results in order: min/max folds are associative (for equal values the same
+    // element wins whatever the grouping), so the bounds are bit-identical.
+    void updateNodeBounds(int64_t idx) {
         const int64_t first = B.leftFirst[idx], cnt = B.count[idx];
-        for (int64_t i = 0; i < cnt; ++i) {
-            const int64_t p = B.primIdx[first + i];
-            mn = vmin(mn, d3(P.bmin[3 * p], P.bmin[3 * p + 1], P.bmin[3 * p + 2]));
-            mx = vmax(mx, d3(P.bmax[3 * p], P.bmax[3 * p + 1], P.bmax[3 * p + 2]));
-        }
+        const int T = par_chunks(cnt);
+        std::vector<D3> mnv(T, d3(kInf, kInf, kInf)), mxv(T, d3(-kInf, -kInf, -kInf));
+        run_chunks(T, [&](int k) {
+            D3 mn = d3(kInf, kInf, kInf), mx = d3(-kInf, -kInf, -kInf);
+            for (int64_t i = cnt * k / T, e = cnt * (k + 1) / T; i < e; ++i) {
+                const int64_t p = B.primIdx[first + i];
+                mn = vmin(mn, d3(P.bmin[3 * p], P.bmin[3 * p + 1], P.bmin[3 * p + 2]));
+                mx = vmax(mx, d3(P.bmax[3 * p], P.bmax[3 * p + 1], P.bmax[3 * p + 2]));
+            }
+            mnv[k] = mn; mxv[k] = mx;
+        });
+        D3 mn = d3(kInf, kInf, kInf), mx = d3(-kInf, -kInf, -kInf);
+        for (int k = 0; k < T; ++k) { mn = vmin(mn, mnv[k]); mx = vmax(mx, mxv[k]); }
         B.lo[3 * idx] = mn.x; B.lo[3 * idx + 1] = mn.y; B.lo[3 * idx + 2] = mn.z;
         B.hi[3 * idx] = mx.x; B.hi[3 * idx + 1] = mx.y; B.hi[3 * idx + 2] = mx.z;
     }
@@ -68,34 +103,59 @@ struct Builder {
     // returns bestAxis/bestPos exactly as findBestSplitPlane (BVH.swift:192-250)
     void findBestSplitPlane(int64_t first, int64_t count, int& axis, double& splitPos) {
         double bestCost = kInf;
+        const int T = par_chunks(count);
+        // centroid bounds (Swift.min/max folds), per chunk then in order
+        std::vector<double> cpart(6 * T);
+        run_chunks(T, [&](int k) {
+            double mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+            for (int64_t i = count * k / T, e = count * (k + 1) / T; i < e; ++i) {
+                const double* c = &P.cen[3 * B.primIdx[first + i]];
+                for (int a = 0; a < 3; ++a) { mn[a] = smin(mn[a], c[a]); mx[a] = smax(mx[a], c[a]); }
+            }
+            for (int a = 0; a < 3; ++a) { cpart[6 * k + a] = mn[a]; cpart[6 * k + 3 + a] = mx[a]; }
+        });
         double cmin[3] = {kInf, kInf, kInf}, cmax[3] = {-kInf, -kInf, -kInf};
-        for (int64_t i = 0; i < count; ++i) {
-            const double* c = &P.cen[3 * B.primIdx[first + i]];
-            for (int a = 0; a < 3; ++a) { cmin[a] = smin(cmin[a], c[a]); cmax[a] = smax(cmax[a], c[a]); }
-        }
+        for (int k = 0; k < T; ++k)
+            for (int a = 0; a < 3; ++a) { cmin[a] = smin(cmin[a], cpart[6 * k + a]); cmax[a] = smax(cmax[a], cpart[6 * k + 3 + a]); }
         bool valid[3];
         double scale[3];
         for (int a = 0; a < 3; ++a) {
             valid[a] = !(cmax[a] <= cmin[a]);
             scale[a] = valid[a] ? double(N) / (cmax[a] - cmin[a]) : 0.0;
-            for (int b = 0; b < N; ++b) {
-                binCnt[a * N + b] = 0;
-                for (int k = 0; k < 3; ++k) { binLo[(a * N + b) * 3 + k] = kInf; binHi[(a * N + b) * 3 + k] = -kInf; }
-            }
         }
-        for (int64_t i = 0; i < count; ++i) {
-            const int64_t p = B.primIdx[first + i];
-            const double* c = &P.cen[3 * p];
-            const double* pl = &P.bmin[3 * p];
-            const double* ph = &P.bmax[3 * p];
-            for (int a = 0; a < 3; ++a) {
-                if (!valid[a]) continue;
-                int64_t q = (int64_t)((c[a] - cmin[a]) * scale[a]);
-                int64_t idx = (q < (int64_t)(N - 1)) ? q : (int64_t)(N - 1);
-                binCnt[a * N + idx] += 1;
-                double* bl = &binLo[(a * N + idx) * 3];
-                double* bh = &binHi[(a * N + idx) * 3];
-                for (int k = 0; k < 3; ++k) { bl[k] = std::fmin(bl[k], pl[k]); bh[k] = std::fmax(bh[k], ph[k]); }
+        // binning, per chunk into private bins, merged in chunk order
+        const int NB = 3 * N;
+        std::vector<int64_t> cntP((size_t)T * NB, 0);
+        std::vector<double> loP((size_t)T * NB * 3, kInf), hiP((size_t)T * NB * 3, -kInf);
+        run_chunks(T, [&](int k) {
+            int64_t* bc = &cntP[(size_t)k * NB];
+            double* blo = &loP[(size_t)k * NB * 3];
+            double* bhi = &hiP[(size_t)k * NB * 3];
+            for (int64_t i = count * k / T, e = count * (k + 1) / T; i < e; ++i) {
+                const int64_t p = B.primIdx[first + i];
+                const double* c = &P.cen[3 * p];
+                const double* pl = &P.bmin[3 * p];
+                const double* ph = &P.bmax[3 * p];
+                for (int a = 0; a < 3; ++a) {
+                    if (!valid[a]) continue;
+                    int64_t q = (int64_t)((c[a] - cmin[a]) * scale[a]);
+                    int64_t idx = (q < (int64_t)(N - 1)) ? q : (int64_t)(N - 1);
+                    bc[a * N + idx] += 1;
+                    double* bl = &blo[(a * N + idx) * 3];
+                    double* bh = &bhi[(a * N + idx) * 3];
+                    for (int kk = 0; kk < 3; ++kk) { bl[kk] = std::fmin(bl[kk], pl[kk]); bh[kk] = std::fmax(bh[kk], ph[kk]); }
+                }
+            }
+        });
+        for (int b = 0; b < NB; ++b) {
+            binCnt[b] = 0;
+            for (int kk = 0; kk < 3; ++kk) { binLo[b * 3 + kk] = kInf; binHi[b * 3 + kk] = -kInf; }
+            for (int k = 0; k < T; ++k) {
+                binCnt[b] += cntP[(size_t)k * NB + b];
+                for (int kk = 0; kk < 3; ++kk) {
+                    binLo[b * 3 + kk] = std::fmin(binLo[b * 3 + kk], loP[((size_t)k * NB + b) * 3 + kk]);
+                    binHi[b * 3 + kk] = std::fmax(binHi[b * 3 + kk], hiP[((size_t)k * NB + b) * 3 + kk]);
+                }
             }
         }
         double leftArea[64], rightArea[64];
@@ -128,30 +188,66 @@ struct Builder {
             }
         }
     }
-    void subdivide(int64_t nodeIdx) {                                     // :128-188
-        const int64_t primCount = B.count[nodeIdx];
-        if (primCount <= maxLeaf && nodeIdx != 0) return;
-        int bestAxis = 0; double bestPos = 0;
-        const int64_t first = B.leftFirst[nodeIdx];
-        findBestSplitPlane(first, primCount, bestAxis, bestPos);
-        int64_t i = first, j = i + primCount - 1;
-        while (i <= j) {
-            if (P.cen[3 * B.primIdx[i] + bestAxis] < bestPos) i += 1;
-            else { std::swap(B.primIdx[i], B.primIdx[j]); j -= 1; }
-        }
-        const int64_t leftCount = i - first;
-        if (leftCount == 0 || leftCount == primCount) return;
-        const int64_t leftChild = ++B.nodesUsed;
-        const int64_t rightChild = ++B.nodesUsed;
-        B.leftFirst[leftChild] = first; B.count[leftChild] = leftCount;
-        B.leftFirst[rightChild] = i; B.count[rightChild] = primCount - leftCount;
-        B.leftFirst[nodeIdx] = leftChild; B.count[nodeIdx] = 0;
-        updateNodeBounds(leftChild);
-        updateNodeBounds(rightChild);
-        subdivide(leftChild);
-        subdivide(rightChild);
-    }
+    // subdivide (BVH.swift:128-188).  Node numbering differs from the reference's
+    // depth-first `nodesUsed` counter - nothing downstream sees it (layout and hash walk
+    // the structure) - so that subtrees can be built concurrently: the node covering prim
+    // range [f, f+c) places its two children at slots D, D+1 and hands its left child the
+    // descendant slots [D+2, D+2cl) and its right child [D+2cl, D+2c-2) (a subtree over c
+    // prims has at most 2c-2 descendants).  Slot assignment depends only on the ranges,
+    // so the result is independent of scheduling.
+    void subdivide(int64_t nodeIdx, int64_t D);
 };
+
+// Concurrency budget for subtree builds (MYRT_BUILD_THREADS, default: hardware threads).
+static std::atomic<int> g_build_slots{-1};
+static bool take_build_slot() {
+    int cur = g_build_slots.load();
+    if (cur < 0) {
+        const int n = build_threads() - 1;                            // the calling thread is one
+        g_build_slots.compare_exchange_strong(cur, n);
+        cur = g_build_slots.load();
+    }
+    while (cur > 0)
+        if (g_build_slots.compare_exchange_weak(cur, cur - 1)) return true;
+    return false;
+}
+static void give_build_slot() { g_build_slots.fetch_add(1); }
+constexpr int64_t kParallelSubtree = 16384;   // prims below which a subtree stays on its thread
+
+void Builder::subdivide(int64_t nodeIdx, int64_t D) {
+    const int64_t primCount = B.count[nodeIdx];
+    if (primCount <= maxLeaf && nodeIdx != 0) return;
+    int bestAxis = 0; double bestPos = 0;
+    const int64_t first = B.leftFirst[nodeIdx];
+    findBestSplitPlane(first, primCount, bestAxis, bestPos);
+    int64_t i = first, j = i + primCount - 1;
+    while (i <= j) {
+        if (P.cen[3 * B.primIdx[i] + bestAxis] < bestPos) i += 1;
+        else { std::swap(B.primIdx[i], B.primIdx[j]); j -= 1; }
+    }
+    const int64_t leftCount = i - first;
+    if (leftCount == 0 || leftCount == primCount) return;
+    const int64_t leftChild = D;
+    const int64_t rightChild = D + 1;
+    B.leftFirst[leftChild] = first; B.count[leftChild] = leftCount;
+    B.leftFirst[rightChild] = i; B.count[rightChild] = primCount - leftCount;
+    B.leftFirst[nodeIdx] = leftChild; B.count[nodeIdx] = 0;
+    updateNodeBounds(leftChild);
+    updateNodeBounds(rightChild);
+    const int64_t dLeft = D + 2, dRight = D + 2 * leftCount;
+    if (primCount - leftCount >= kParallelSubtree && take_build_slot()) {
+        std::thread t([this, rightChild, dRight] {
+            Builder sub(P, B, maxLeaf, N);
+            sub.subdivide(rightChild, dRight);
+            give_build_slot();
+        });
+        subdivide(leftChild, dLeft);
+        t.join();
+    } else {
+        subdivide(leftChild, dLeft);
+        subdivide(rightChild, dRight);
+    }
+}
 }  // namespace
 
 RefBVH build_ref_bvh(const PrimSet& prims, int maxLeaf, int binCount) {
@@ -165,7 +261,8 @@ RefBVH build_ref_bvh(const PrimSet& prims, int maxLeaf, int binCount) {
     B.leftFirst[0] = 0; B.count[0] = n; B.nodesUsed = 0;
     Builder bld(prims, B, maxLeaf, binCount);
     bld.updateNodeBounds(0);
-    bld.subdivide(0);
+    bld.subdivide(0, 1);
+    B.nodesUsed = B.count[0] == 0 && n > 0 ? 2 * n - 2 : 0;   // > 0 iff the root was split
     return B;
 }
 
@@ -347,6 +444,11 @@ static int32_t layout_bvh(const RefBVH& b, std::vector<WRec>& recs, EmitLeaf emi
 
 int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err) {
     auto t0 = std::chrono::steady_clock::now();
+    const bool trace = std::getenv("MYRT_BUILD_TRACE") != nullptr;   // phase timings on stderr
+    auto phase = [&](const char* name) {
+        if (trace) std::fprintf(stderr, "[build] %-10s %9.1f ms\n", name,
+                                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
     S.eps = d->intersection_test_epsilon;
     S.shadow_eps = d->shadow_ray_epsilon;
     S.background[0] = d->background_color.x; S.background[1] = d->background_color.y; S.background[2] = d->background_color.z;
@@ -497,6 +599,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             Nn = o.normals; off = o.indices_one_based ? 1 : 0;
             if ((nPos > 0 && !P) || (nIdx > 0 && !I)) { err = "mesh arrays missing"; return RT_ERR_INVALID_ARG; }
         }
+        phase("ply");
         const bool isSmooth = o.smooth != 0;
         const int64_t triCount = nIdx / 3;
         for (int64_t t = 0; t < 3 * triCount; ++t) {
@@ -517,10 +620,13 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         std::vector<D3> faceN;
         if (!Nn) {
             faceN.resize(triCount);
-            for (int64_t t = 0; t < triCount; ++t) {
-                D3 v0 = pos(I[3 * t] - off), v1 = pos(I[3 * t + 1] - off), v2 = pos(I[3 * t + 2] - off);
-                faceN[t] = normalize(cross(v1 - v0, v2 - v0));
-            }
+            const int TF = std::max(1, std::min<int>(build_threads(), (int)(triCount / 65536)));
+            run_chunks(TF, [&](int kc) {
+                for (int64_t t = triCount * kc / TF, tEnd = triCount * (kc + 1) / TF; t < tEnd; ++t) {
+                    D3 v0 = pos(I[3 * t] - off), v1 = pos(I[3 * t + 1] - off), v2 = pos(I[3 * t + 2] - off);
+                    faceN[t] = normalize(cross(v1 - v0, v2 - v0));
+                }
+            });
             if (isSmooth) {
                 vtx.assign(nPos, d3(0, 0, 0));
                 for (int64_t t = 0; t < triCount; ++t)
@@ -528,8 +634,11 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
                 for (auto& v : vtx) v = normalize(v);
             }
         }
+        phase("normals");
         triangles.resize(start + triCount);
-        for (int64_t t = 0; t < triCount; ++t) {
+        const int TC = std::max(1, std::min<int>(build_threads(), (int)(triCount / 65536)));
+        run_chunks(TC, [&](int kc) {                      // independent per triangle
+        for (int64_t t = triCount * kc / TC, tEnd = triCount * (kc + 1) / TC; t < tEnd; ++t) {
             const int64_t i0 = I[3 * t] - off, i1 = I[3 * t + 1] - off, i2 = I[3 * t + 2] - off;
             Tri& tr = triangles[start + t];
             tr.v0 = pos(i0); tr.v1 = pos(i1); tr.v2 = pos(i2);
@@ -556,6 +665,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             bb.prims.cen[3 * t] = c.x; bb.prims.cen[3 * t + 1] = c.y; bb.prims.cen[3 * t + 2] = c.z;
             bb.triIndex[t] = start + t;
         }
+        });
         if (std::find(meshOrder.begin(), meshOrder.end(), o.id) == meshOrder.end()) meshOrder.push_back(o.id);
         if (triCount > 0) {
             blases.push_back(std::move(bb));
@@ -589,6 +699,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         insts.push_back(ib);
     }
 
+    phase("flatten");
     // ---- BLAS builds (buildBLASForMesh: maxLeaf 2, SAH, 12 bins; RTContext.swift:430-435)
     int64_t maxBlasDepth = 0;
     for (auto& bb : blases) {
@@ -598,7 +709,15 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         maxBlasDepth = std::max(maxBlasDepth, bb.depth);
     }
 
+    phase("blas_bvh");
     // ---- device layout: BLAS records + leaf-ordered triangles
+    {
+        size_t nt = 0, nr = 0;
+        for (const auto& bb : blases) { nt += bb.triIndex.size(); nr += bb.triIndex.size(); }
+        S.tris.reserve(nt);
+        S.normals.reserve(9 * nt);
+        S.recs.reserve(nr + insts.size() + 1);
+    }
     for (auto& bb : blases) {
         auto emit = [&](int64_t firstSlot, int64_t count) -> int64_t {
             const int64_t first = (int64_t)S.tris.size();
@@ -626,6 +745,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
     }
     S.blas_records = (int64_t)S.recs.size();
 
+    phase("layout");
     // ---- instances (makeInstance, RTContext.swift:437-457) and TLAS (buildTLAS :459-474)
     PrimSet tp;
     tp.n = (int64_t)insts.size();
@@ -727,6 +847,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
     }
     if (S.recs.size() >= (size_t)INT32_MAX || S.tris.size() >= (size_t)INT32_MAX) { err = "scene too large for int32 refs"; return RT_ERR_UNSUPPORTED; }
     if (maxBlasDepth + 1 > 63) { err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550)"; return RT_ERR_STACK; }
+    phase("tlas+inst");
     S.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
 }
