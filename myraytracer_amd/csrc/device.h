@@ -300,10 +300,9 @@ __device__ __forceinline__ bool prim_shadow(int kind, const TriRec& T, const V3&
 // (true), or the caller must pop (false).  Order = near first, ties to L (the reference
 // pushes R then L after `if d1 > d2 swap`, RTContext.swift:600-606); the far child is
 // pushed.  Children beyond `lim` (conservative t-pruning) count as misses.
-template <bool COUNT, bool FAST, bool SHADOW>
-__device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
-                                           Stack& st, Counts& c) {
-    const WRec& R = P.recs[ref];
+template <bool COUNT, bool FAST, bool SHADOW, class Rec>
+__device__ __forceinline__ bool inner_step_rec(const RenderParams& P, const Rec& R, int& ref, const V3& o,
+                                               const V3& inv, double lim, Stack& st, Counts& c) {
     if (COUNT) c.recs++;
     double t0, t1;
     bool h0 = slab_hit<FAST>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv, P.eps, t0);
@@ -332,6 +331,57 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
     if (h0) { ref = a; return true; }
     if (h1) { ref = b; return true; }
     return false;
+}
+
+// A record held in SGPRs: loaded with scalar loads when every active lane of the wave is
+// at the same node.  Vector loads of one node by 64 lanes return 64 copies through the
+// texture-data path (7 instructions x 1 KB per wave step), which profiling showed ~90%
+// busy (TD_TD_BUSY); the scalar path moves the 104 B once, through the scalar cache.
+struct SRec {
+    double lo[2][3], hi[2][3];
+    int ref[2];
+};
+typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double dpair(unsigned lo, unsigned hi) {
+    return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+__device__ __forceinline__ SRec load_rec_scalar(const WRec* pv) {
+    // the address is wave-uniform; make that explicit so it lives in SGPRs
+    const unsigned long long av = (unsigned long long)pv;
+    const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
+    const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
+    const WRec* p = (const WRec*)((unsigned long long)alo | ((unsigned long long)ahi << 32));
+    u32x16 a;
+    u32x8 b;
+    u32x2 r;
+    asm volatile(
+        "s_load_dwordx16 %0, %3, 0x0\n\t"
+        "s_load_dwordx8 %1, %3, 0x40\n\t"
+        "s_load_dwordx2 %2, %3, 0x60\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(a), "=&s"(b), "=&s"(r)   // early-clobber: outputs must not overlap the address
+        : "s"(p));
+    SRec R;
+    R.lo[0][0] = dpair(a[0], a[1]);   R.lo[0][1] = dpair(a[2], a[3]);   R.lo[0][2] = dpair(a[4], a[5]);
+    R.lo[1][0] = dpair(a[6], a[7]);   R.lo[1][1] = dpair(a[8], a[9]);   R.lo[1][2] = dpair(a[10], a[11]);
+    R.hi[0][0] = dpair(a[12], a[13]); R.hi[0][1] = dpair(a[14], a[15]); R.hi[0][2] = dpair(b[0], b[1]);
+    R.hi[1][0] = dpair(b[2], b[3]);   R.hi[1][1] = dpair(b[4], b[5]);   R.hi[1][2] = dpair(b[6], b[7]);
+    R.ref[0] = (int)r[0];
+    R.ref[1] = (int)r[1];
+    return R;
+}
+
+template <bool COUNT, bool FAST, bool SHADOW>
+__device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
+                                           Stack& st, Counts& c) {
+    const int r0 = __builtin_amdgcn_readfirstlane(ref);
+    if (P.scalar_nodes && __all(ref == r0)) {
+        const SRec R = load_rec_scalar(P.recs + r0);
+        return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
+    }
+    return inner_step_rec<COUNT, FAST, SHADOW>(P, P.recs[ref], ref, o, inv, lim, st, c);
 }
 
 // Pop the next node whose entry distance does not exceed `lim`; false when the stack

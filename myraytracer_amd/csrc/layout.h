@@ -103,7 +103,7 @@ struct RenderParams {
     int32_t stack_depth;             // LDS stack entries per lane
     int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
-    int32_t pad1;
+    int32_t scalar_nodes;            // wave-uniform records via scalar loads (device.h inner_step)
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)

@@ -416,6 +416,8 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     {
         const char* xe = std::getenv("MYRT_XCD");                // tile-group size per XCD (device.h xcd_tile)
         P.xcd_remap = xe ? std::atoi(xe) : 0;
+        const char* se = std::getenv("MYRT_SCALAR");            // A/B switch: MYRT_SCALAR=0
+        P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
