@@ -373,14 +373,56 @@ __device__ __forceinline__ SRec load_rec_scalar(const WRec* pv) {
     return R;
 }
 
+struct SCRec {                       // a CRec held in SGPRs
+    float lo[2][3], hi[2][3];
+    int ref[2];
+};
+__device__ __forceinline__ float lo_f(unsigned long long q) { return __builtin_bit_cast(float, (unsigned)q); }
+__device__ __forceinline__ float hi_f(unsigned long long q) { return __builtin_bit_cast(float, (unsigned)(q >> 32)); }
+__device__ __forceinline__ SCRec load_crec_scalar(const CRec* pv) {
+    const unsigned long long av = (unsigned long long)pv;
+    const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
+    const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
+    const CRec* p = (const CRec*)((unsigned long long)alo | ((unsigned long long)ahi << 32));
+    // 64-bit outputs: element extraction from a 16-dword ext_vector SGPR output was
+    // miscompiled (all float/int elements read as element 0); register pairs are not
+    unsigned long long q0, q1, q2, q3, q4, q5, q6;
+    asm volatile(
+        "s_load_dwordx2 %0, %7, 0x0\n\t"
+        "s_load_dwordx2 %1, %7, 0x8\n\t"
+        "s_load_dwordx2 %2, %7, 0x10\n\t"
+        "s_load_dwordx2 %3, %7, 0x18\n\t"
+        "s_load_dwordx2 %4, %7, 0x20\n\t"
+        "s_load_dwordx2 %5, %7, 0x28\n\t"
+        "s_load_dwordx2 %6, %7, 0x30\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(q0), "=&s"(q1), "=&s"(q2), "=&s"(q3), "=&s"(q4), "=&s"(q5), "=&s"(q6)
+        : "s"(p));
+    SCRec R;
+    R.lo[0][0] = lo_f(q0); R.lo[0][1] = hi_f(q0); R.lo[0][2] = lo_f(q1);
+    R.lo[1][0] = hi_f(q1); R.lo[1][1] = lo_f(q2); R.lo[1][2] = hi_f(q2);
+    R.hi[0][0] = lo_f(q3); R.hi[0][1] = hi_f(q3); R.hi[0][2] = lo_f(q4);
+    R.hi[1][0] = hi_f(q4); R.hi[1][1] = lo_f(q5); R.hi[1][2] = hi_f(q5);
+    R.ref[0] = (int)(unsigned)q6;
+    R.ref[1] = (int)(unsigned)(q6 >> 32);
+    return R;
+}
+
+// One inner record: compact (float32 bounds, exact) below P.compact_limit, else full;
+// through the scalar cache when the whole wave is at this node.
 template <bool COUNT, bool FAST, bool SHADOW>
 __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
                                            Stack& st, Counts& c) {
     const int r0 = __builtin_amdgcn_readfirstlane(ref);
     if (P.scalar_nodes && __all(ref == r0)) {
+        if (r0 < P.compact_limit) {
+            const SCRec R = load_crec_scalar(P.crecs + r0);
+            return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
+        }
         const SRec R = load_rec_scalar(P.recs + r0);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
     }
+    if (ref < P.compact_limit) return inner_step_rec<COUNT, FAST, SHADOW>(P, P.crecs[ref], ref, o, inv, lim, st, c);
     return inner_step_rec<COUNT, FAST, SHADOW>(P, P.recs[ref], ref, o, inv, lim, st, c);
 }
 

@@ -30,6 +30,17 @@ struct alignas(128) WRec {
 };
 static_assert(sizeof(WRec) == 128, "WRec must be one 128-B line");
 
+// BLAS record with float32 bounds, used when every BLAS bound is exactly a float (always
+// true for PLY meshes without motion blur: positions are float32 widened to double,
+// PLYReader.swift:85-102, and node bounds are min/max of vertex coordinates).  Widening
+// back to double is exact, so the FP64 slab test sees the same values from half the bytes.
+struct alignas(64) CRec {
+    float lo[2][3], hi[2][3];
+    int32_t ref[2];
+    int32_t pad[2];
+};
+static_assert(sizeof(CRec) == 64, "CRec is one 64-B half line");
+
 struct alignas(16) TriRec {
     double v0[3], e1[3], e2[3];
     int32_t last;         // 1 = last triangle of its leaf
@@ -81,6 +92,7 @@ struct DCamera {
 
 struct RenderParams {
     const WRec* recs;
+    const CRec* crecs;               // compact copy of records [0, compact_limit)
     const TriRec* tris;
     const double* normals;
     const DInstance* insts;
@@ -104,6 +116,8 @@ struct RenderParams {
     int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
     int32_t scalar_nodes;            // wave-uniform records via scalar loads (device.h inner_step)
+    int32_t compact_limit;           // records below this index are read from crecs
+    int32_t pad2;
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)

@@ -256,6 +256,7 @@ static int32_t fail(int32_t code, const std::string& msg) { g_err = msg; return 
 struct DeviceReplica {
     int device = 0;
     WRec* recs = nullptr;
+    CRec* crecs = nullptr;
     TriRec* tris = nullptr;
     double* normals = nullptr;
     DInstance* insts = nullptr;
@@ -295,7 +296,7 @@ static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
 static void free_replica(DeviceReplica& r) {
     (void)hipSetDevice(r.device);
     wave_release(r.wave);
-    (void)hipFree(r.recs); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
+    (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
@@ -309,6 +310,7 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r) {
     HIP_TRY(hipSetDevice(device));
     int32_t rc;
     if ((rc = upload(S.recs, &r.recs, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.crecs, &r.crecs, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.normals, &r.normals, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
@@ -393,7 +395,7 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
                                 double* out_rgb, uint8_t* out_rgba8) {
     const HostScene& S = s->host;
     RenderParams P{};
-    P.recs = r.recs; P.tris = r.tris; P.normals = r.normals; P.insts = r.insts; P.tlas_leaf = r.tlas_leaf;
+    P.recs = r.recs; P.crecs = r.crecs; P.tris = r.tris; P.normals = r.normals; P.insts = r.insts; P.tlas_leaf = r.tlas_leaf;
     P.mats = r.mats; P.plights = r.plights;
     for (int k = 0; k < 3; ++k) { P.tlas_root_lo[k] = S.tlas_root_lo[k]; P.tlas_root_hi[k] = S.tlas_root_hi[k]; }
     P.tlas_root_ref = S.tlas_root_ref;
@@ -418,6 +420,8 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         P.xcd_remap = xe ? std::atoi(xe) : 0;
         const char* se = std::getenv("MYRT_SCALAR");            // A/B switch: MYRT_SCALAR=0
         P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
+        const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0
+        P.compact_limit = (ce && ce[0] == '0') ? 0 : (int32_t)S.compact_records;
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
@@ -529,6 +533,7 @@ int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32
         s->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         // device copies are authoritative; drop the large host arrays
         s->host.recs.clear(); s->host.recs.shrink_to_fit();
+        s->host.crecs.clear(); s->host.crecs.shrink_to_fit();
         s->host.tris.clear(); s->host.tris.shrink_to_fit();
         s->host.normals.clear(); s->host.normals.shrink_to_fit();
         *out = s;

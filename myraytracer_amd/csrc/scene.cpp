@@ -744,6 +744,27 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         bb.prims = PrimSet();
     }
     S.blas_records = (int64_t)S.recs.size();
+    {   // compact BLAS records when every bound survives a float32 round trip exactly
+        bool exact = true;
+        for (int64_t q = 0; q < S.blas_records && exact; ++q)
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 3; ++k) {
+                    const double lo = S.recs[q].lo[c][k], hi = S.recs[q].hi[c][k];
+                    exact &= (double)(float)lo == lo && (double)(float)hi == hi;
+                }
+        if (exact && S.blas_records > 0) {
+            S.crecs.resize(S.blas_records);
+            for (int64_t q = 0; q < S.blas_records; ++q) {
+                CRec& r = S.crecs[q];
+                std::memset(&r, 0, sizeof(r));
+                for (int c = 0; c < 2; ++c) {
+                    for (int k = 0; k < 3; ++k) { r.lo[c][k] = (float)S.recs[q].lo[c][k]; r.hi[c][k] = (float)S.recs[q].hi[c][k]; }
+                    r.ref[c] = S.recs[q].ref[c];
+                }
+            }
+            S.compact_records = S.blas_records;
+        }
+    }
 
     phase("layout");
     // ---- instances (makeInstance, RTContext.swift:437-457) and TLAS (buildTLAS :459-474)

@@ -53,6 +53,8 @@ struct HostScene {
     bool has_dielectric = false;
     // ---- device layout (host copies)
     std::vector<WRec> recs;
+    std::vector<CRec> crecs;               // float32-bound copy of the BLAS records (if exact)
+    int64_t compact_records = 0;           // crecs.size() (kept after the host copy is dropped)
     std::vector<TriRec> tris;
     std::vector<double> normals;           // 9 per TriRec
     std::vector<DInstance> insts;
