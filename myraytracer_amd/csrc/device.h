@@ -704,6 +704,18 @@ __device__ __forceinline__ void hit_geometry(const RenderParams& P, const V3& o,
     if (I.det_neg) Ngeo = -Ngeo;
 }
 
+// Blinn-Phong lobe pow(NdotH, shininess) for 0 <= NdotH <= 1 and shininess >= 1 (the
+// point-light term, Object+Extension.swift:134-137): exp2(shininess * log2(NdotH)).  OCML
+// pow carries an extended-precision log for correct rounding in every range and needs far
+// more registers; here the result differs from pow by a few ulps (relative ~1e-14, vs
+// the 1e-5 parity bar) and NdotH = 0 / 1 give exactly 0 / 1.
+// Not inlined on purpose: inlined, the polynomial constants of log2/exp2 were hoisted
+// to the kernel prologue and spilled to scratch once per lane (~0.3 GB of scratch
+// writes per C3 frame); as a call they are materialized where they are used.
+__device__ __noinline__ double phong_pow(double x, double y) {
+    return exp2(y * log2(x));
+}
+
 // orthonormalBasis (Object+Extension.swift:531-552)
 __device__ __forceinline__ void onb(V3 n, V3& tangent, V3& bitangent) {
     const double sign = n.z >= 0 ? 1.0 : -1.0;

@@ -78,7 +78,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                     const V3 view = normalize(-d);
                     const V3 hv = normalize(wi + view);
                     const double NdotH = smax(0.0, dot(N, hv));
-                    const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
+                    const V3 Ls = ld3(M.specular) * phong_pow(NdotH, shininess);
                     const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
                     contrib = (Ld + Ls) * atten;
                 }
