@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--scaling", default="weak", choices=["strong", "weak"],
                    help="strong: one frame tile-partitioned over ranks (C4); weak: every rank renders a full frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-path", action="store_true", help="skip the rt_render (host buffer) measurement")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
     p.add_argument("--cache", default=os.path.join(ROOT, "scenes_cache"))
@@ -171,6 +172,24 @@ def main():
                              "load_bytes": int(128 * wc.records_fetched + 80 * wc.tri_tests
                                                + 72 * wc.normal_fetches + 24 * wc.pixels)}}
 
+    # ---- host-buffer path (rt_render: render + D2H of the FP64 framebuffer + host scatter,
+    # batches overlapped with the copies).  Reported next to `value`, never as `value`.
+    host_path = None
+    if not args.no_host_path:
+        try:
+            import numpy as np
+            host_buf = np.zeros((rows, W, 3), dtype=np.float64)        # caller-owned, reused
+            eng.render_rows(0, first, step, False, out=host_buf)        # staging warm-up
+            t_h = time.perf_counter()
+            nh = 5
+            for _ in range(nh):
+                eng.render_rows(0, first, step, False, out=host_buf)
+            ms_h = (time.perf_counter() - t_h) * 1e3 / nh
+            host_path = {"ms_per_frame": round(ms_h, 4), "value": round(rays_rank / (ms_h * 1e-3) / 1e6, 2),
+                         "unit": "Mrays/s", "what": "rt_render wall time incl. D2H of the FP64 RGB framebuffer"}
+        except Exception as e:  # pragma: no cover
+            log("host path failed:", e)
+
     # ---- CPU baseline (rank 0, N = 1 only): oracle on a bounded sample of the same frame
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -195,6 +214,7 @@ def main():
                        "secondary_rays_per_frame": rays_secondary if world == 1 else None},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "host_path": host_path,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -253,6 +253,8 @@ static int32_t fail(int32_t code, const std::string& msg) { g_err = msg; return 
         if (_e != hipSuccess) return fail(RT_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
 
+constexpr int kRenderBatches = 8;   // rt_render: chunk batches per replica (progress / overlap granularity)
+
 struct DeviceReplica {
     int device = 0;
     WRec* recs = nullptr;
@@ -270,7 +272,12 @@ struct DeviceReplica {
     int64_t cap_px = 0;
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;        // rt_render: D2H of finished batches
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // rt_render staging (grown on demand, reused across calls)
+    double* out_d = nullptr; uint8_t* out8_d = nullptr; int64_t out_cap_px = 0;
+    double* host_rgb = nullptr; uint8_t* host_rgba = nullptr; int64_t host_cap_px = 0;   // pinned
+    std::vector<hipEvent_t> batch_done, batch_copied;
     int64_t bytes = 0;
     WaveBuffers wave;                         // wavefront-pipeline queues (grown on demand)
 };
@@ -302,6 +309,12 @@ static void free_replica(DeviceReplica& r) {
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.stream) (void)hipStreamDestroy(r.stream);
+    if (r.copy_stream) (void)hipStreamDestroy(r.copy_stream);
+    (void)hipFree(r.out_d); (void)hipFree(r.out8_d);
+    if (r.host_rgb) (void)hipHostFree(r.host_rgb);
+    if (r.host_rgba) (void)hipHostFree(r.host_rgba);
+    for (auto e : r.batch_done) (void)hipEventDestroy(e);
+    for (auto e : r.batch_copied) (void)hipEventDestroy(e);
     r = DeviceReplica();
 }
 
@@ -321,6 +334,13 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r) {
     if ((rc = upload(S.jitter, &r.jitter, r.bytes)) != RT_OK) return rc;
     HIP_TRY(hipMalloc((void**)&r.counters, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&r.copy_stream, hipStreamNonBlocking));
+    r.batch_done.resize(kRenderBatches);
+    r.batch_copied.resize(kRenderBatches);
+    for (int b = 0; b < kRenderBatches; ++b) {
+        HIP_TRY(hipEventCreateWithFlags(&r.batch_done[b], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&r.batch_copied[b], hipEventDisableTiming));
+    }
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
     return RT_OK;
@@ -621,9 +641,13 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
     return RT_OK;
 }
 
-// Host-buffer render across all device replicas: chunk k of the selection goes to
-// replica (k mod D); each replica renders its share into device memory, copies it back
-// and the host scatters its rows into the packed output (no collective involved).
+// Host-buffer render across all device replicas (Renderer.render + renderRGBA8Async,
+// Object+Extension.swift:52-379, RayTracer.swift:137-205).  Chunk k of the selection goes to
+// replica (k mod D).  Each replica renders its chunks in up to kRenderBatches launches on its
+// compute stream while a copy stream moves finished batches into pinned staging, so PCIe
+// transfer overlaps rendering; the calling thread scatters finished rows into the caller's
+// buffer, reports progress after every batch and honours cancellation at batch granularity
+// (the reference's cancel was a no-op).  No collective is involved.
 int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb, uint8_t* out_rgba8,
                   rt_stats* stats, rt_progress_fn progress, void* user) {
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
@@ -640,64 +664,152 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
     const int32_t D = (int32_t)s->devs.size();
     std::vector<int32_t> rowOff(sel.size() + 1, 0);
     for (size_t q = 0; q < sel.size(); ++q) rowOff[q + 1] = rowOff[q] + std::min(8, H - 8 * sel[q]);
-    std::vector<int32_t> codes(D, RT_OK);
-    std::vector<std::string> errs(D);
-    std::vector<double> kms(D, 0.0);
-    std::vector<unsigned long long> shadow(D, 0), secondary(D, 0);
-    auto work = [&](int32_t k) {
+    const int32_t rowsTotal = rowOff.back();
+
+    // ---- per replica: its chunk list, batch plan, buffers; enqueue everything
+    struct Plan { int32_t myFirst, myStep, nChunks, rows, nb, per; std::vector<int32_t> batchRow; };
+    std::vector<Plan> plan(D);
+    for (int32_t k = 0; k < D; ++k) {
         DeviceReplica& r = s->devs[k];
-        auto body = [&]() -> int32_t {
-            HIP_TRY(hipSetDevice(r.device));
-            const int32_t myFirst = first + k * step, myStep = step * D;
-            const int32_t rows = rt_rows_for_chunks(H, myFirst, myStep);
-            if (rows == 0) return RT_OK;
-            double* d_rgb = nullptr; uint8_t* d_rgba = nullptr;
-            HIP_TRY(hipMalloc((void**)&d_rgb, (size_t)rows * W * 3 * sizeof(double)));
-            if (out_rgba8) HIP_TRY(hipMalloc((void**)&d_rgba, (size_t)rows * W * 4));
-            HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
-            RenderParams P = make_params(s, r, cam, myFirst, myStep, d_rgb, d_rgba);
-            HIP_TRY(hipEventRecord(r.ev0, r.stream));
-            int32_t lrc = launch(s, r, P, r.stream, false);
-            if (lrc != RT_OK) { (void)hipFree(d_rgb); (void)hipFree(d_rgba); return lrc; }
-            HIP_TRY(hipEventRecord(r.ev1, r.stream));
-            std::vector<double> h_rgb((size_t)rows * W * 3);
-            std::vector<uint8_t> h_rgba(out_rgba8 ? (size_t)rows * W * 4 : 0);
-            HIP_TRY(hipMemcpyAsync(h_rgb.data(), d_rgb, h_rgb.size() * sizeof(double), hipMemcpyDeviceToHost, r.stream));
-            if (out_rgba8) HIP_TRY(hipMemcpyAsync(h_rgba.data(), d_rgba, h_rgba.size(), hipMemcpyDeviceToHost, r.stream));
-            unsigned long long c[kCounterWords];
-            HIP_TRY(hipMemcpyAsync(c, r.counters, sizeof(c), hipMemcpyDeviceToHost, r.stream));
-            HIP_TRY(hipStreamSynchronize(r.stream));
-            float ms = 0; (void)hipEventElapsedTime(&ms, r.ev0, r.ev1);
-            kms[k] = ms; shadow[k] = c[0]; secondary[k] = c[1];
-            (void)hipFree(d_rgb); (void)hipFree(d_rgba);
-            // scatter: my q-th chunk is selection entry k + q*D
-            int32_t srcRow = 0;
-            for (size_t q = k; q < sel.size(); q += D) {
-                const int32_t nr = rowOff[q + 1] - rowOff[q];
-                if (out_rgb) std::memcpy(out_rgb + (size_t)rowOff[q] * W * 3, h_rgb.data() + (size_t)srcRow * W * 3, (size_t)nr * W * 3 * sizeof(double));
-                if (out_rgba8) std::memcpy(out_rgba8 + (size_t)rowOff[q] * W * 4, h_rgba.data() + (size_t)srcRow * W * 4, (size_t)nr * W * 4);
-                srcRow += nr;
-            }
-            return RT_OK;
-        };
-        codes[k] = body();
-        errs[k] = g_err;
-    };
-    if (D == 1) work(0);
-    else {
-        std::vector<std::thread> th;
-        for (int32_t k = 0; k < D; ++k) th.emplace_back(work, k);
-        for (auto& t : th) t.join();
+        Plan& pl = plan[k];
+        pl.myFirst = first + k * step; pl.myStep = step * D;
+        pl.nChunks = 0;
+        for (int32_t c = pl.myFirst; c < num_chunks_total(H); c += pl.myStep) pl.nChunks++;
+        pl.rows = rt_rows_for_chunks(H, pl.myFirst, pl.myStep);
+        if (pl.nChunks == 0) { pl.nb = 0; continue; }
+        pl.per = (pl.nChunks + kRenderBatches - 1) / kRenderBatches;
+        pl.nb = (pl.nChunks + pl.per - 1) / pl.per;
+        pl.batchRow.assign(pl.nb + 1, 0);
+        for (int32_t b = 0; b < pl.nb; ++b) {
+            const int32_t c0 = pl.myFirst + b * pl.per * pl.myStep;
+            const int32_t nc = std::min(pl.per, pl.nChunks - b * pl.per);
+            pl.batchRow[b + 1] = pl.batchRow[b] + rt_rows_for_chunks(H, c0, pl.myStep) -
+                                 rt_rows_for_chunks(H, c0 + nc * pl.myStep, pl.myStep);
+        }
+        HIP_TRY(hipSetDevice(r.device));
+        const int64_t px = (int64_t)pl.rows * W;
+        if (px > r.out_cap_px) {
+            (void)hipFree(r.out_d); (void)hipFree(r.out8_d); r.out_d = nullptr; r.out8_d = nullptr; r.out_cap_px = 0;
+            HIP_TRY(hipMalloc((void**)&r.out_d, px * 3 * sizeof(double)));
+            HIP_TRY(hipMalloc((void**)&r.out8_d, px * 4));
+            r.out_cap_px = px;
+        }
+        if (px > r.host_cap_px) {
+            if (r.host_rgb) (void)hipHostFree(r.host_rgb);
+            if (r.host_rgba) (void)hipHostFree(r.host_rgba);
+            r.host_rgb = nullptr; r.host_rgba = nullptr; r.host_cap_px = 0;
+            HIP_TRY(hipHostMalloc((void**)&r.host_rgb, px * 3 * sizeof(double), hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&r.host_rgba, px * 4, hipHostMallocDefault));
+            r.host_cap_px = px;
+        }
+        HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
+        HIP_TRY(hipEventRecord(r.ev0, r.stream));
     }
-    for (int32_t k = 0; k < D; ++k) if (codes[k] != RT_OK) return fail(codes[k], errs[k]);
-    if (progress && !progress(user, rowOff.back(), rowOff.back())) return fail(RT_ERR_CANCELLED, "cancelled");
+    // batch b of every replica is enqueued before batch b-1 is drained: one batch renders
+    // while the previous one is copied and scattered; cancellation stops further launches
+    int32_t maxNb = 0;
+    for (const auto& pl : plan) maxNb = std::max(maxNb, pl.nb);
+    auto enqueue = [&](int32_t b) -> int32_t {
+        for (int32_t k = 0; k < D; ++k) {
+            const Plan& pl = plan[k];
+            if (b >= pl.nb) continue;
+            DeviceReplica& r = s->devs[k];
+            HIP_TRY(hipSetDevice(r.device));
+            const int32_t c0 = pl.myFirst + b * pl.per * pl.myStep;
+            const int32_t nc = std::min(pl.per, pl.nChunks - b * pl.per);
+            double* drgb = r.out_d + (size_t)pl.batchRow[b] * W * 3;
+            uint8_t* drgba = out_rgba8 ? r.out8_d + (size_t)pl.batchRow[b] * W * 4 : nullptr;
+            RenderParams P = make_params(s, r, cam, c0, pl.myStep, drgb, drgba);
+            P.num_chunks = nc;
+            const int32_t lrc = launch(s, r, P, r.stream, false);
+            if (lrc != RT_OK) return lrc;
+            HIP_TRY(hipEventRecord(r.batch_done[b], r.stream));
+            const size_t nrows = (size_t)(pl.batchRow[b + 1] - pl.batchRow[b]);
+            HIP_TRY(hipStreamWaitEvent(r.copy_stream, r.batch_done[b], 0));
+            HIP_TRY(hipMemcpyAsync(r.host_rgb + (size_t)pl.batchRow[b] * W * 3, drgb, nrows * W * 3 * sizeof(double),
+                                   hipMemcpyDeviceToHost, r.copy_stream));
+            if (out_rgba8)
+                HIP_TRY(hipMemcpyAsync(r.host_rgba + (size_t)pl.batchRow[b] * W * 4, drgba, nrows * W * 4,
+                                       hipMemcpyDeviceToHost, r.copy_stream));
+            HIP_TRY(hipEventRecord(r.batch_copied[b], r.copy_stream));
+        }
+        return RT_OK;
+    };
+    if (maxNb > 0 && (rc = enqueue(0)) != RT_OK) return rc;
+    int32_t enqueued = maxNb > 0 ? 1 : 0;
+    // ---- drain: scatter each finished batch, report progress, honour cancellation
+    int32_t rowsDone = 0;
+    bool cancelled = false;
+    for (int32_t b = 0; b < enqueued; ++b) {
+        if (!cancelled && enqueued < maxNb) {
+            if ((rc = enqueue(enqueued)) != RT_OK) return rc;
+            enqueued++;
+        }
+        for (int32_t k = 0; k < D; ++k) {
+            const Plan& pl = plan[k];
+            if (b >= pl.nb) continue;
+            DeviceReplica& r = s->devs[k];
+            HIP_TRY(hipSetDevice(r.device));
+            HIP_TRY(hipEventSynchronize(r.batch_copied[b]));
+            if (cancelled) continue;
+            // replica k's q-th chunk is selection entry k + q*D; chunks are scattered by
+            // several threads (host memcpy bandwidth, not PCIe, bounds this step)
+            const int32_t q0 = b * pl.per, q1 = std::min(pl.nChunks, q0 + pl.per);
+            std::vector<int32_t> src(q1 - q0 + 1, pl.batchRow[b]);
+            for (int32_t q = q0; q < q1; ++q) {
+                const size_t e = (size_t)k + (size_t)q * D;
+                src[q - q0 + 1] = src[q - q0] + (rowOff[e + 1] - rowOff[e]);
+            }
+            auto copy_chunks = [&](int32_t qa, int32_t qb) {
+                for (int32_t q = qa; q < qb; ++q) {
+                    const size_t e = (size_t)k + (size_t)q * D;
+                    const int32_t nr = rowOff[e + 1] - rowOff[e];
+                    const int32_t sr = src[q - q0];
+                    if (out_rgb) std::memcpy(out_rgb + (size_t)rowOff[e] * W * 3, r.host_rgb + (size_t)sr * W * 3,
+                                             (size_t)nr * W * 3 * sizeof(double));
+                    if (out_rgba8) std::memcpy(out_rgba8 + (size_t)rowOff[e] * W * 4, r.host_rgba + (size_t)sr * W * 4,
+                                               (size_t)nr * W * 4);
+                }
+            };
+            const int32_t nq = q1 - q0;
+            const int32_t nt = std::max(1, std::min<int32_t>(nq, (int32_t)std::min(8u, std::thread::hardware_concurrency())));
+            if (nt <= 1 || (int64_t)nq * 8 * W < 65536) {
+                copy_chunks(q0, q1);
+            } else {
+                std::vector<std::thread> th;
+                for (int32_t t = 1; t < nt; ++t)
+                    th.emplace_back(copy_chunks, q0 + nq * t / nt, q0 + nq * (t + 1) / nt);
+                copy_chunks(q0, q0 + nq / nt);
+                for (auto& x : th) x.join();
+            }
+            rowsDone += src.back() - src.front();
+            if (progress && !progress(user, rowsDone, rowsTotal)) cancelled = true;
+        }
+    }
+    for (int32_t k = 0; k < D; ++k) {
+        if (plan[k].nb == 0) continue;
+        HIP_TRY(hipSetDevice(s->devs[k].device));
+        HIP_TRY(hipEventRecord(s->devs[k].ev1, s->devs[k].stream));
+    }
+    double km = 0;
+    int64_t sh = 0, se = 0;
+    for (int32_t k = 0; k < D; ++k) {
+        if (plan[k].nb == 0) continue;
+        DeviceReplica& r = s->devs[k];
+        HIP_TRY(hipSetDevice(r.device));
+        HIP_TRY(hipStreamSynchronize(r.stream));
+        unsigned long long c[kCounterWords];
+        HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
+        sh += (int64_t)c[0]; se += (int64_t)c[1];
+        float ms = 0; (void)hipEventElapsedTime(&ms, r.ev0, r.ev1);
+        km = std::max(km, (double)ms);
+    }
+    if (cancelled) return fail(RT_ERR_CANCELLED, "cancelled");
     if (stats) {
         stats->meshes = s->host.n_meshes; stats->triangles = s->host.n_tris;
         stats->spheres = s->host.n_spheres; stats->planes = s->host.n_planes;
         const int64_t n = (int64_t)std::sqrt((double)std::max(1, C.num_samples));
-        stats->primary_rays = (int64_t)rowOff.back() * W * n * n;
-        int64_t sh = 0, se = 0; double km = 0;
-        for (int32_t k = 0; k < D; ++k) { sh += (int64_t)shadow[k]; se += (int64_t)secondary[k]; km = std::max(km, kms[k]); }
+        stats->primary_rays = (int64_t)rowsTotal * W * n * n;
         stats->shadow_rays = sh; stats->secondary_rays = se; stats->kernel_ms = km;
         stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }

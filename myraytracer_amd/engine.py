@@ -157,15 +157,20 @@ class RayTracerEngine:
 
     # -- rendering
     def render_rows(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
-                    want_rgba: bool = True, progress: Optional[Callable[[RenderProgress], bool]] = None):
-        """Render the selected 8-row chunks; returns (rgb[rows,W,3] f64, rgba[rows,W,4] u8, RenderStats)."""
+                    want_rgba: bool = True, progress: Optional[Callable[[RenderProgress], bool]] = None,
+                    out: Optional[np.ndarray] = None):
+        """Render the selected 8-row chunks; returns (rgb[rows,W,3] f64, rgba[rows,W,4] u8, RenderStats).
+        `out`: optional reusable C-contiguous float64 (rows, W, 3) array for the RGB result."""
         lib = load_library()
         if not (0 <= camera_index < len(self.scene.cameras)):
             raise RenderError(A.RT_ERR_INVALID_CAMERA, "Invalid camera index")
         cam = self.scene.cameras[camera_index]
         W, H = max(1, int(cam.image_resolution[0])), max(1, int(cam.image_resolution[1]))
         rows = lib.rt_rows_for_chunks(H, chunk_first, chunk_step)
-        rgb = np.empty((rows, W, 3), dtype=np.float64)
+        if out is not None and out.shape == (rows, W, 3) and out.dtype == np.float64 and out.flags.c_contiguous:
+            rgb = out
+        else:
+            rgb = np.empty((rows, W, 3), dtype=np.float64)
         rgba = np.empty((rows, W, 4), dtype=np.uint8) if want_rgba else None
         st = A.rt_stats()
 

@@ -126,3 +126,22 @@ def test_c5_10m_mirrors_sampled_chunks(scene_dir):
     assert np.array_equal(rgba, ref8)
     assert (st.shadow_rays, st.secondary_rays) == (ost.shadow_rays, ost.secondary_rays)
     assert st.secondary_rays > 0
+
+
+def test_progress_per_batch_and_cancel():
+    """rt_render reports progress after every finished batch of chunks and honours
+    cancellation (the reference's progress closure returns Bool, RayTracer.swift:115-131;
+    SURVEY.md §8b: cancel at chunk granularity)."""
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 160, 200)      # 25 chunks -> 7 batches
+    eng = M.RayTracerEngine(sc)
+    seen = []
+    r = eng.render(0, progress=lambda p: seen.append(p.fraction) or True)
+    assert len(seen) >= 2 and seen == sorted(seen) and seen[-1] == 1.0
+    ref = oracle.OracleScene(sc).render(0, threads=0)[0]
+    assert float(np.abs(r.rgb - ref).max()) <= TOL
+    calls = []
+    with pytest.raises(M.RenderError) as e:
+        eng.render(0, progress=lambda p: calls.append(p.fraction) or False)
+    assert e.value.code == -60 and len(calls) == 1
+    again = eng.render(0)                                            # the engine stays usable
+    assert np.array_equal(again.rgb, r.rgb)
