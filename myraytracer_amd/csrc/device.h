@@ -207,11 +207,23 @@ __device__ __forceinline__ bool finite3(const V3& a) {
     return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
 }
 
+// Triangle geometry from either record format (layout.h TriRec / CTri).
+__device__ __forceinline__ void tri_geom(const TriRec& T, V3& v0, V3& e1, V3& e2) {
+    v0 = ld3(T.v0); e1 = ld3(T.e1); e2 = ld3(T.e2);
+}
+__device__ __forceinline__ void tri_geom(const CTri& T, V3& v0, V3& e1, V3& e2) {
+    v0 = v3((double)T.v0[0], (double)T.v0[1], (double)T.v0[2]);
+    e1 = v3((double)T.v1[0], (double)T.v1[1], (double)T.v1[2]) - v0;   // = host e1 = v1 - v0
+    e2 = v3((double)T.v2[0], (double)T.v2[1], (double)T.v2[2]) - v0;
+}
+
 // Closest-hit triangle test, intersectTriangle (RTContext.swift:479-510) minus the
 // hit-point/normal writes, which are recomputed once for the final hit (same values).
-__device__ __forceinline__ bool tri_closest(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double eps,
+template <class Tri>
+__device__ __forceinline__ bool tri_closest(const Tri& T, const V3& o_mb, const V3& d, double tlo, double eps,
                                            Hit& h, int triIdx, int instIdx) {
-    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+    V3 v0, e1, e2;
+    tri_geom(T, v0, e1, e2);
     const V3 pvec = cross(d, e2);
     const double det = dot(e1, pvec);
     if (fabs(det) < eps) return false;
@@ -228,9 +240,11 @@ __device__ __forceinline__ bool tri_closest(const TriRec& T, const V3& o_mb, con
     return true;
 }
 // triShadowHit (RTContext.swift:832-848)
-__device__ __forceinline__ bool tri_shadow(const TriRec& T, const V3& o_mb, const V3& d, double tlo, double thi,
+template <class Tri>
+__device__ __forceinline__ bool tri_shadow(const Tri& T, const V3& o_mb, const V3& d, double tlo, double thi,
                                            double eps) {
-    const V3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+    V3 v0, e1, e2;
+    tri_geom(T, v0, e1, e2);
     const V3 pvec = cross(d, e2);
     const double det = dot(e1, pvec);
     if (fabs(det) < eps) return false;
@@ -497,13 +511,16 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
                 const V3 omb = ol - ld3(I.tri_motion) * time;   // Triangle.motionBlur offset (:480-481)
                 const int inst = le.inst;
                 auto blas_leaf = [&](int r) -> bool {
-                    for (int t = ~r;; ++t) {
-                        const TriRec& T = P.tris[t];
-                        if (COUNT) c.tris++;
-                        const bool closer = tri_closest(T, omb, dl, tlo, eps, h, t, inst);
-                        if (MYRT_REF(P) && closer && I.smooth) c.smooth++;
-                        if (T.last) break;
-                    }
+                    auto run = [&](const auto* tris) {
+                        for (int t = ~r;; ++t) {
+                            const auto& T = tris[t];
+                            if (COUNT) c.tris++;
+                            const bool closer = tri_closest(T, omb, dl, tlo, eps, h, t, inst);
+                            if (MYRT_REF(P) && closer && I.smooth) c.smooth++;
+                            if (T.last) break;
+                        }
+                    };
+                    if (P.ctris) run(P.ctris); else run(P.tris);
                     return false;
                 };
                 const int sbase = st.sp;
@@ -552,13 +569,16 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
                                 ol, il, eps, dr) && !(dr > lim)) {
                 const V3 omb = ol - ld3(I.tri_motion) * time;
                 auto blas_leaf = [&](int r) -> bool {
-                    for (int t = ~r;; ++t) {
-                        const TriRec& T = P.tris[t];
-                        if (COUNT) c.tris++;
-                        if (tri_shadow(T, omb, dl, 0.0, tmax, eps)) return true;
-                        if (T.last) break;
-                    }
-                    return false;
+                    auto run = [&](const auto* tris) -> bool {
+                        for (int t = ~r;; ++t) {
+                            const auto& T = tris[t];
+                            if (COUNT) c.tris++;
+                            if (tri_shadow(T, omb, dl, 0.0, tmax, eps)) return true;
+                            if (T.last) break;
+                        }
+                        return false;
+                    };
+                    return P.ctris ? run(P.ctris) : run(P.tris);
                 };
                 const int sbase = st.sp;
                 bool hit;
@@ -597,16 +617,20 @@ __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Sta
     } else {
         const int e = ~ref;
         if (e < P.tlas_leaf_base) {                                  // BLAS leaf run
-            for (int t = e;; ++t) {
-                const TriRec& T = P.tris[t];
-                if (COUNT) c.tris++;
-                if (SHADOW) {
-                    if (tri_shadow(T, o, d, 0.0, tmax, eps)) return 2;
-                } else {
-                    tri_closest(T, o, d, tlo, eps, h, t, T.prim);     // prim = owning instance
+            auto run = [&](const auto* tris) -> bool {
+                for (int t = e;; ++t) {
+                    const auto& T = tris[t];
+                    if (COUNT) c.tris++;
+                    if (SHADOW) {
+                        if (tri_shadow(T, o, d, 0.0, tmax, eps)) return true;
+                    } else {
+                        tri_closest(T, o, d, tlo, eps, h, t, T.prim); // prim = owning instance
+                    }
+                    if (T.last) break;
                 }
-                if (T.last) break;
-            }
+                return false;
+            };
+            if (P.ctris ? run(P.ctris) : run(P.tris)) return 2;
         } else {                                                      // TLAS leaf: instance list
             const int k0 = e - P.tlas_leaf_base;
             int k1 = k0;

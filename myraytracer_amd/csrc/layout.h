@@ -48,6 +48,18 @@ struct alignas(16) TriRec {
 };
 static_assert(sizeof(TriRec) == 80, "TriRec is 80 B");
 
+// Leaf-ordered triangle with float32 vertices, used when every vertex is exactly a float
+// (PLY meshes).  The kernel rebuilds e1 = v1 - v0 and e2 = v2 - v0 in FP64 from the
+// widened vertices - the same operation on the same values as the host's TriRec edges
+// (RTContext.swift:204-208), so the MT test sees identical edges from 48 B instead of 80 B.
+struct alignas(16) CTri {
+    float v0[3], v1[3], v2[3];
+    int32_t last;
+    int32_t prim;
+    int32_t pad;
+};
+static_assert(sizeof(CTri) == 48, "CTri is 48 B");
+
 struct DMaterial {        // ParsingKit Material fields used by trace()
     double ambient[3], diffuse[3], specular[3], mirror[3], absorption[3];
     double phong, ior, absorption_index, roughness;
@@ -93,6 +105,7 @@ struct DCamera {
 struct RenderParams {
     const WRec* recs;
     const CRec* crecs;               // compact copy of records [0, compact_limit)
+    const CTri* ctris;               // compact triangles (nullptr = use tris)
     const TriRec* tris;
     const double* normals;
     const DInstance* insts;

@@ -259,6 +259,7 @@ struct DeviceReplica {
     int device = 0;
     WRec* recs = nullptr;
     CRec* crecs = nullptr;
+    CTri* ctris = nullptr;
     TriRec* tris = nullptr;
     double* normals = nullptr;
     DInstance* insts = nullptr;
@@ -303,7 +304,7 @@ static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
 static void free_replica(DeviceReplica& r) {
     (void)hipSetDevice(r.device);
     wave_release(r.wave);
-    (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
+    (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
@@ -324,6 +325,7 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r) {
     int32_t rc;
     if ((rc = upload(S.recs, &r.recs, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.crecs, &r.crecs, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.ctris, &r.ctris, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.normals, &r.normals, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
@@ -442,6 +444,8 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
         const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0
         P.compact_limit = (ce && ce[0] == '0') ? 0 : (int32_t)S.compact_records;
+        const char* te = std::getenv("MYRT_CTRI");              // A/B switch: MYRT_CTRI=0
+        P.ctris = (S.compact_tris && !(te && te[0] == '0')) ? r.ctris : nullptr;
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
@@ -554,6 +558,7 @@ int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32
         // device copies are authoritative; drop the large host arrays
         s->host.recs.clear(); s->host.recs.shrink_to_fit();
         s->host.crecs.clear(); s->host.crecs.shrink_to_fit();
+        s->host.ctris.clear(); s->host.ctris.shrink_to_fit();
         s->host.tris.clear(); s->host.tris.shrink_to_fit();
         s->host.normals.clear(); s->host.normals.shrink_to_fit();
         *out = s;

@@ -744,6 +744,29 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         bb.prims = PrimSet();
     }
     S.blas_records = (int64_t)S.recs.size();
+    if (!S.has_special && !S.tris.empty()) {   // compact triangles when every vertex is a float
+        bool exact = true;
+        auto fx = [](double x) { return (double)(float)x == x; };
+        for (size_t q = 0; q < S.tris.size() && exact; ++q) {
+            const Tri& t = triangles[S.tris[q].prim];
+            exact &= fx(t.v0.x) && fx(t.v0.y) && fx(t.v0.z) && fx(t.v1.x) && fx(t.v1.y) && fx(t.v1.z) &&
+                     fx(t.v2.x) && fx(t.v2.y) && fx(t.v2.z);
+        }
+        if (exact) {
+            S.ctris.resize(S.tris.size());
+            for (size_t q = 0; q < S.tris.size(); ++q) {
+                const Tri& t = triangles[S.tris[q].prim];
+                CTri& c = S.ctris[q];
+                c.v0[0] = (float)t.v0.x; c.v0[1] = (float)t.v0.y; c.v0[2] = (float)t.v0.z;
+                c.v1[0] = (float)t.v1.x; c.v1[1] = (float)t.v1.y; c.v1[2] = (float)t.v1.z;
+                c.v2[0] = (float)t.v2.x; c.v2[1] = (float)t.v2.y; c.v2[2] = (float)t.v2.z;
+                c.last = S.tris[q].last;
+                c.prim = S.tris[q].prim;          // rewritten below in identity mode
+                c.pad = 0;
+            }
+            S.compact_tris = true;
+        }
+    }
     {   // compact BLAS records when every bound survives a float32 round trip exactly
         bool exact = true;
         for (int64_t q = 0; q < S.blas_records && exact; ++q)
@@ -862,7 +885,10 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         if (ident) {
             for (size_t i = 0; i < insts.size(); ++i) {
                 const BlasBuild& bb = blases[insts[i].blas];
-                for (int64_t t = bb.tri_first; t < bb.tri_end; ++t) S.tris[t].prim = (int32_t)i;
+                for (int64_t t = bb.tri_first; t < bb.tri_end; ++t) {
+                    S.tris[t].prim = (int32_t)i;
+                    if (S.compact_tris) S.ctris[t].prim = (int32_t)i;
+                }
             }
         }
     }

@@ -56,6 +56,8 @@ struct HostScene {
     std::vector<CRec> crecs;               // float32-bound copy of the BLAS records (if exact)
     int64_t compact_records = 0;           // crecs.size() (kept after the host copy is dropped)
     std::vector<TriRec> tris;
+    std::vector<CTri> ctris;               // float32-vertex copy of tris (if every vertex is exact)
+    bool compact_tris = false;
     std::vector<double> normals;           // 9 per TriRec
     std::vector<DInstance> insts;
     std::vector<DTlasLeafEntry> tlas_leaf;
