@@ -167,6 +167,9 @@ def main():
                 "alg_bytes_per_ray": round(alg_bytes / max(1, rays_rank), 1),
                 "alg_counts": {"node_fetches": int(wc.ref_node_fetches), "tri_tests": int(wc.ref_tri_tests),
                                "smooth_hits": int(wc.ref_smooth_hits), "pixels": int(wc.ref_pixels)},
+                "simd_efficiency": {
+                    "closest": round(wc.lane_steps_closest / max(1, 64 * wc.wave_steps_closest), 3),
+                    "shadow": round(wc.lane_steps_shadow / max(1, 64 * wc.wave_steps_shadow), 3)},
                 "executed": {"records_128B": int(wc.records_fetched), "tri_tests": int(wc.tri_tests),
                              "normal_fetches": int(wc.normal_fetches), "pixels": int(wc.pixels),
                              "load_bytes": int(128 * wc.records_fetched + 80 * wc.tri_tests

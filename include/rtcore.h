@@ -212,6 +212,10 @@ typedef struct rt_work_counters {
     int64_t ref_tri_tests;      /* Moeller-Trumbore tests                             */
     int64_t ref_smooth_hits;    /* closer smooth hits (normal triple interpolated)    */
     int64_t ref_pixels;         /* pixels written                                     */
+    /* SIMD efficiency of the traversal loops (megakernel, identity scenes): iterations run
+     * by lanes vs iterations run by their waves (64 x the max over the wave's lanes).     */
+    int64_t lane_steps_closest, wave_steps_closest;
+    int64_t lane_steps_shadow, wave_steps_shadow;
 } rt_work_counters;
 int32_t rt_render_device_counted(rt_scene* scene, int32_t device_slot, int32_t camera_index,
                                  int32_t chunk_first, int32_t chunk_step,

@@ -76,7 +76,9 @@ class rt_work_counters(C.Structure):
     _fields_ = [("records_fetched", C.c_int64), ("tri_tests", C.c_int64), ("normal_fetches", C.c_int64),
                 ("instance_entries", C.c_int64), ("pixels", C.c_int64),
                 ("ref_node_fetches", C.c_int64), ("ref_tri_tests", C.c_int64),
-                ("ref_smooth_hits", C.c_int64), ("ref_pixels", C.c_int64)]
+                ("ref_smooth_hits", C.c_int64), ("ref_pixels", C.c_int64),
+                ("lane_steps_closest", C.c_int64), ("wave_steps_closest", C.c_int64),
+                ("lane_steps_shadow", C.c_int64), ("wave_steps_shadow", C.c_int64)]
 
 
 class rt_ply_mesh(C.Structure):

@@ -168,6 +168,7 @@ struct Stack {
 struct Counts {
     unsigned shadow, secondary;
     unsigned long long recs, tris, normals, insts, nodes, smooth;
+    unsigned long long it_closest, it_shadow;   // loop iterations of this lane (divergence study)
 };
 constexpr int kMissRef = 0x7fffffff;   // count_ref any-hit: a pushed child whose slab test missed
 
@@ -666,7 +667,7 @@ __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3
                                                  double tlo, Hit& h, Stack& st, Counts& c) {
     int ref;
     if (!unified_begin(P, o, inv, DINF, ref)) return;   // the stack is empty here (base 0)
-    while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0) {}
+    do { if (COUNT) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0);
 }
 template <bool COUNT>
 __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
@@ -684,7 +685,7 @@ __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     const int base = st.sp;
     int r;
-    while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0) {}
+    do { if (COUNT) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0);
     st.sp = base;
     return r == 2;
 }
@@ -761,6 +762,11 @@ __device__ __forceinline__ V3 fresnel_conductor(double eta, double k, double cos
     return 0.5 * (Rs + Rp);
 }
 
+__device__ __forceinline__ unsigned long long wave_max(unsigned long long x) {   // all 64 lanes active
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) { const unsigned long long y = __shfl_xor(x, off, 64); x = y > x ? y : x; }
+    return x;
+}
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     const int j = chunk * 8 + rowInChunk;
     const DCamera& C = P.cam;
     const bool valid = (i < C.width) && (j < C.height);
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (valid) {
         MYRT_STACK(st, lds_stack);
         PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
@@ -233,6 +233,13 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
         }
         const unsigned long long ff = wave_sum(cnt.nodes), gg = wave_sum(cnt.smooth);
         if (lane == 0 && P.count_ref) { atomicAdd(&P.counters[7], ff); atomicAdd(&P.counters[8], gg); }
+        // divergence study: lane iterations vs the wave's (max over lanes) iterations
+        const unsigned long long lc = wave_sum(cnt.it_closest), wc = wave_max(cnt.it_closest);
+        const unsigned long long ls = wave_sum(cnt.it_shadow), ws = wave_max(cnt.it_shadow);
+        if (lane == 0 && !P.count_ref) {
+            atomicAdd(&P.counters[9], lc); atomicAdd(&P.counters[10], wc);
+            atomicAdd(&P.counters[11], ls); atomicAdd(&P.counters[12], ws);
+        }
     }
 }
 
@@ -642,6 +649,8 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
         out->instance_entries = (int64_t)c[5]; out->pixels = (int64_t)c[6];
         out->ref_node_fetches = (int64_t)q[7]; out->ref_tri_tests = (int64_t)q[3];
         out->ref_smooth_hits = (int64_t)q[8]; out->ref_pixels = (int64_t)q[6];
+        out->lane_steps_closest = (int64_t)c[9]; out->wave_steps_closest = (int64_t)c[10];
+        out->lane_steps_shadow = (int64_t)c[11]; out->wave_steps_shadow = (int64_t)c[12];
     }
     return RT_OK;
 }

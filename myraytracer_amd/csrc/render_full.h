@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void k_events(RenderParams P) {
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
     if (i >= P.cam.width || j >= P.cam.height) return;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     MYRT_STACK(st, lds_stack);
     long long events = 0;
     (void)pixel_full<false, true>(P, i, j, events, st, cnt);
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void render_full(RenderParams P) {
     full_pixel_of(P, i, j, slot, row);
     const bool valid = (i < P.cam.width) && (j < P.cam.height);
     const int lane = threadIdx.x & 63;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (valid) {
         MYRT_STACK(st, lds_stack);
         const size_t o = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void k_persist(WaveParams W, int64_t N, unsign
     const RenderParams& P = W.R;
     constexpr bool SHADOW = (MODE == 2);
     MYRT_STACK(st, lds_stack);
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const int lane = lane_id();
     const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     WaveWork w{0, 0, (int)(blockIdx.x & 7), 0, false};
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void k_general(WaveParams W, int64_t N) {
     extern __shared__ unsigned long long lds_stack[];
     const RenderParams& P = W.R;
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned rays = 0;
     V3 o, d;
     double tlo, tmax, time;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void k_shade(WaveParams W) {
     const int depth = W.depth;
     const int64_t path = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (path >= W.P) return;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const int L = P.num_plights;
     bool active;
     TraceItem it;
