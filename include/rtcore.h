@@ -242,6 +242,17 @@ uint64_t rt_debug_bvh_hash(const rt_scene* scene, int32_t instance);
 int32_t  rt_debug_host_build(const rt_scene_desc* desc, uint64_t* hashes, int32_t max_hashes,
                              int32_t* n_instances, rt_scene_info* info);
 
+/* Explicit-ray queries on device `slot` through the render kernels' traversal (host
+ * arrays, n rays; o/d: 3 doubles per ray).  rt_debug_trace_rays = intersectTLAS
+ * (RTContext.swift:619-720) with tMin: out_t (+inf on a miss), world hit point, world
+ * geometric normal (before facing), materialOverride (-1 on a miss).
+ * rt_debug_occluded_rays = occludedTLAS (:724-781) with tMax: out[i] = 1 if blocked.   */
+int32_t rt_debug_trace_rays(rt_scene* scene, int32_t slot, int32_t n, const double* o, const double* d,
+                            const double* tmin, const double* time, double* out_t, double* out_p,
+                            double* out_n, int32_t* out_mat);
+int32_t rt_debug_occluded_rays(rt_scene* scene, int32_t slot, int32_t n, const double* o, const double* d,
+                               const double* tmax, const double* time, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

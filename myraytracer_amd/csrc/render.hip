@@ -246,6 +246,52 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 }  // namespace dev
 }  // namespace myrt
 
+namespace myrt {
+namespace dev {
+// Explicit-ray queries (rt_debug_trace_rays / rt_debug_occluded_rays): the render kernels'
+// walks on caller-given rays, one lane per ray.
+struct RayBatch {
+    const double *o, *d, *tlim, *time;
+    double *out_t, *out_p, *out_n;
+    int32_t* out_mat;
+    uint8_t* out_occ;
+    int32_t n, uni;
+};
+__global__ __launch_bounds__(256) void k_trace_rays(RenderParams P, RayBatch B) {
+    extern __shared__ unsigned long long lds_stack[];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B.n) return;
+    MYRT_STACK(st, lds_stack);
+    Counts c{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const V3 o = v3(B.o[3 * i], B.o[3 * i + 1], B.o[3 * i + 2]), d = v3(B.d[3 * i], B.d[3 * i + 1], B.d[3 * i + 2]);
+    const double time = B.time[i];
+    Hit h;
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    if (P.has_tlas) {
+        if (B.uni) uni_closest<false>(P, o, d, rcp(d), B.tlim[i], h, st, c);
+        else intersect_closest<false>(P, o, d, rcp(d), B.tlim[i], time, h, st, c);
+    }
+    V3 p = v3(0, 0, 0), n = v3(0, 0, 0);
+    if (h.inst >= 0) hit_geometry<false>(P, o, d, time, h, p, n, c);
+    B.out_t[i] = h.inst >= 0 ? h.t : DINF;
+    B.out_p[3 * i] = p.x; B.out_p[3 * i + 1] = p.y; B.out_p[3 * i + 2] = p.z;
+    B.out_n[3 * i] = n.x; B.out_n[3 * i + 1] = n.y; B.out_n[3 * i + 2] = n.z;
+    B.out_mat[i] = h.inst >= 0 ? P.insts[h.inst].material : -1;
+}
+__global__ __launch_bounds__(256) void k_occluded_rays(RenderParams P, RayBatch B) {
+    extern __shared__ unsigned long long lds_stack[];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B.n) return;
+    MYRT_STACK(st, lds_stack);
+    Counts c{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const V3 o = v3(B.o[3 * i], B.o[3 * i + 1], B.o[3 * i + 2]), d = v3(B.d[3 * i], B.d[3 * i + 1], B.d[3 * i + 2]);
+    const bool hit = B.uni ? uni_occluded<false>(P, o, d, B.tlim[i], st, c)
+                           : occluded<false>(P, o, d, B.tlim[i], B.time[i], st, c);
+    B.out_occ[i] = hit ? 1 : 0;
+}
+}  // namespace dev
+}  // namespace myrt
+
 // ================================================================== host side / C ABI
 using namespace myrt;
 
@@ -888,6 +934,78 @@ int32_t rt_debug_host_build(const rt_scene_desc* desc, uint64_t* hashes, int32_t
     } catch (const std::exception& e) {
         return fail(RT_ERR_INVALID_ARG, e.what());
     }
+}
+
+// ---- debug: explicit rays through the render kernels' traversal
+static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o, const double* d, const double* tl,
+                          const double* time, double* out_t, double* out_p, double* out_n, int32_t* out_mat,
+                          uint8_t* out_occ) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
+    if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
+    if (n < 0 || (n > 0 && (!o || !d || !tl || !time))) return fail(RT_ERR_INVALID_ARG, "bad ray arrays");
+    if (n == 0) return RT_OK;
+    std::lock_guard<std::mutex> lock(s->mu);
+    DeviceReplica& r = s->devs[slot];
+    HIP_TRY(hipSetDevice(r.device));
+    RenderParams P = make_params(s, r, 0, 0, 1, nullptr, nullptr);
+    dev::RayBatch B{};
+    B.n = n;
+    const char* ue = std::getenv("MYRT_UNIFIED");
+    B.uni = (P.identity && P.has_tlas && !(ue && ue[0] == '0')) ? 1 : 0;
+    std::vector<void*> allocs;
+    auto dalloc = [&](size_t bytes, void** p) -> int32_t {
+        HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 8)));
+        allocs.push_back(*p);
+        return RT_OK;
+    };
+    int32_t rc = RT_OK;
+    double *dO, *dD, *dL, *dT;
+    if ((rc = dalloc((size_t)n * 24, (void**)&dO)) || (rc = dalloc((size_t)n * 24, (void**)&dD)) ||
+        (rc = dalloc((size_t)n * 8, (void**)&dL)) || (rc = dalloc((size_t)n * 8, (void**)&dT))) {
+        for (void* p : allocs) (void)hipFree(p);
+        return rc;
+    }
+    HIP_TRY(hipMemcpy(dO, o, (size_t)n * 24, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dD, d, (size_t)n * 24, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dL, tl, (size_t)n * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dT, time, (size_t)n * 8, hipMemcpyHostToDevice));
+    B.o = dO; B.d = dD; B.tlim = dL; B.time = dT;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    const size_t lds = (size_t)dev::kLds * 256 * sizeof(unsigned long long);
+    if (out_occ) {
+        if ((rc = dalloc((size_t)n, (void**)&B.out_occ)) != RT_OK) { for (void* p : allocs) (void)hipFree(p); return rc; }
+        hipLaunchKernelGGL(dev::k_occluded_rays, grid, block, lds, r.stream, P, B);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(r.stream));
+        HIP_TRY(hipMemcpy(out_occ, B.out_occ, (size_t)n, hipMemcpyDeviceToHost));
+    } else {
+        if ((rc = dalloc((size_t)n * 8, (void**)&B.out_t)) || (rc = dalloc((size_t)n * 24, (void**)&B.out_p)) ||
+            (rc = dalloc((size_t)n * 24, (void**)&B.out_n)) || (rc = dalloc((size_t)n * 4, (void**)&B.out_mat))) {
+            for (void* p : allocs) (void)hipFree(p);
+            return rc;
+        }
+        hipLaunchKernelGGL(dev::k_trace_rays, grid, block, lds, r.stream, P, B);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(r.stream));
+        HIP_TRY(hipMemcpy(out_t, B.out_t, (size_t)n * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(out_p, B.out_p, (size_t)n * 24, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(out_n, B.out_n, (size_t)n * 24, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(out_mat, B.out_mat, (size_t)n * 4, hipMemcpyDeviceToHost));
+    }
+    for (void* p : allocs) (void)hipFree(p);
+    return RT_OK;
+}
+
+int32_t rt_debug_trace_rays(rt_scene* s, int32_t slot, int32_t n, const double* o, const double* d,
+                            const double* tmin, const double* time, double* out_t, double* out_p, double* out_n,
+                            int32_t* out_mat) {
+    if (n > 0 && (!out_t || !out_p || !out_n || !out_mat)) return fail(RT_ERR_INVALID_ARG, "bad output arrays");
+    return debug_rays(s, slot, n, o, d, tmin, time, out_t, out_p, out_n, out_mat, nullptr);
+}
+int32_t rt_debug_occluded_rays(rt_scene* s, int32_t slot, int32_t n, const double* o, const double* d,
+                               const double* tmax, const double* time, uint8_t* out) {
+    if (n > 0 && !out) return fail(RT_ERR_INVALID_ARG, "bad output array");
+    return debug_rays(s, slot, n, o, d, tmax, time, nullptr, nullptr, nullptr, nullptr, out);
 }
 
 // ---- debug: canonical BVH hashes (tests compare them with the oracle's)

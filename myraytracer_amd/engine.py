@@ -220,8 +220,39 @@ class RayTracerEngine:
                                                        C.byref(wc)))
         return wc
 
+    def trace_rays(self, origins, dirs, tmin=None, time=None, slot: int = 0):
+        """Closest hits of explicit rays through the render kernels' traversal
+        (rt_debug_trace_rays): returns t (+inf = miss), world point, world normal, material."""
+        o, d, n, tl, tm = _ray_arrays(origins, dirs, tmin, time)
+        t = np.empty(n); p = np.empty((n, 3)); nn = np.empty((n, 3)); mat = np.empty(n, np.int32)
+        _check(load_library().rt_debug_trace_rays(
+            self._h, slot, n, o.ctypes.data_as(A.c_double_p), d.ctypes.data_as(A.c_double_p),
+            tl.ctypes.data_as(A.c_double_p), tm.ctypes.data_as(A.c_double_p), t.ctypes.data_as(A.c_double_p),
+            p.ctypes.data_as(A.c_double_p), nn.ctypes.data_as(A.c_double_p), mat.ctypes.data_as(A.c_int32_p)))
+        return t, p, nn, mat
+
+    def occluded_rays(self, origins, dirs, tmax, time=None, slot: int = 0):
+        """Any-hit of explicit segments (rt_debug_occluded_rays): bool per ray."""
+        o, d, n, tl, tm = _ray_arrays(origins, dirs, tmax, time)
+        out = np.empty(n, np.uint8)
+        _check(load_library().rt_debug_occluded_rays(
+            self._h, slot, n, o.ctypes.data_as(A.c_double_p), d.ctypes.data_as(A.c_double_p),
+            tl.ctypes.data_as(A.c_double_p), tm.ctypes.data_as(A.c_double_p), out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out.astype(bool)
+
     def bvh_hash(self, instance: int) -> int:
         return int(load_library().rt_debug_bvh_hash(self._h, instance))
+
+
+def _ray_arrays(origins, dirs, tlim, time):
+    o = np.ascontiguousarray(origins, dtype=np.float64).reshape(-1, 3)
+    d = np.ascontiguousarray(dirs, dtype=np.float64).reshape(-1, 3)
+    n = o.shape[0]
+    if d.shape[0] != n:
+        raise ValueError("origins and dirs differ in length")
+    tl = np.zeros(n) if tlim is None else np.ascontiguousarray(np.broadcast_to(tlim, (n,)), dtype=np.float64)
+    tm = np.zeros(n) if time is None else np.ascontiguousarray(np.broadcast_to(time, (n,)), dtype=np.float64)
+    return o, d, n, tl, tm
 
 
 def rows_for_chunks(height: int, chunk_first: int, chunk_step: int) -> int:

@@ -58,6 +58,11 @@ def lib() -> C.CDLL:
         L.oracle_hit_aabb.restype = C.c_double
         L.oracle_intersect_triangle.argtypes = [d3, d3, d3, d3, d3, C.c_double, C.c_double, d3, d3]
         L.oracle_intersect_triangle.restype = C.c_double
+        i32 = C.POINTER(C.c_int32)
+        L.oracle_trace_rays.argtypes = [C.c_void_p, C.c_int32, d3, d3, d3, d3, d3, d3, d3, i32]
+        L.oracle_trace_rays.restype = C.c_int32
+        L.oracle_occluded_rays.argtypes = [C.c_void_p, C.c_int32, d3, d3, d3, d3, C.POINTER(C.c_uint8)]
+        L.oracle_occluded_rays.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -109,6 +114,32 @@ class OracleScene:
 
     def num_instances(self):
         return int(lib().oracle_num_instances(self._h))
+
+    @staticmethod
+    def _rays(origins, dirs, tlim, time):
+        o = np.ascontiguousarray(origins, dtype=np.float64).reshape(-1, 3)
+        d = np.ascontiguousarray(dirs, dtype=np.float64).reshape(-1, 3)
+        n = o.shape[0]
+        tl = np.zeros(n) if tlim is None else np.ascontiguousarray(np.broadcast_to(tlim, (n,)), dtype=np.float64)
+        tm = np.zeros(n) if time is None else np.ascontiguousarray(np.broadcast_to(time, (n,)), dtype=np.float64)
+        return o, d, n, tl, tm
+
+    def trace_rays(self, origins, dirs, tmin=None, time=None):
+        """intersectTLAS on explicit rays: (t, world point, world normal, material)."""
+        o, d, n, tl, tm = self._rays(origins, dirs, tmin, time)
+        t = np.empty(n); p = np.empty((n, 3)); nn = np.empty((n, 3)); mat = np.empty(n, np.int32)
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        lib().oracle_trace_rays(self._h, n, dp(o), dp(d), dp(tl), dp(tm), dp(t), dp(p), dp(nn),
+                                mat.ctypes.data_as(C.POINTER(C.c_int32)))
+        return t, p, nn, mat
+
+    def occluded_rays(self, origins, dirs, tmax, time=None):
+        """occludedTLAS on explicit segments: bool per ray."""
+        o, d, n, tl, tm = self._rays(origins, dirs, tmax, time)
+        out = np.empty(n, np.uint8)
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        lib().oracle_occluded_rays(self._h, n, dp(o), dp(d), dp(tl), dp(tm), out.ctypes.data_as(C.POINTER(C.c_uint8)))
+        return out.astype(bool)
 
 
 def pcg32_stream(seed: int, n: int):

@@ -1300,4 +1300,35 @@ double oracle_intersect_triangle(const double* v0, const double* v1, const doubl
     return r.hit.t;
 }
 
+// Explicit-ray queries (tests/test_gpu_rays.py): intersectTLAS / occludedTLAS
+// (RTContext.swift:619-781) on caller-given rays, Ray(origin:dir:time:) + tMin / tMax.
+int32_t oracle_trace_rays(void* scene, int32_t n, const double* o, const double* d, const double* tmin,
+                          const double* time, double* out_t, double* out_p, double* out_n, int32_t* out_mat) {
+    using namespace orc;
+    const Context& C = static_cast<OracleScene*>(scene)->C;
+    Counters k;
+    for (int32_t i = 0; i < n; ++i) {
+        Ray r(v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]), time[i]);
+        r.tMin = tmin[i];
+        if (C.hasTlas) intersectTLAS(C, r, C.intersectionTestEpsilon, k);
+        out_t[i] = r.hit.kind == -1 ? kInf : r.hit.t;
+        out_p[3 * i] = r.hit.p.x; out_p[3 * i + 1] = r.hit.p.y; out_p[3 * i + 2] = r.hit.p.z;
+        out_n[3 * i] = r.hit.n.x; out_n[3 * i + 1] = r.hit.n.y; out_n[3 * i + 2] = r.hit.n.z;
+        out_mat[i] = r.hit.kind == -1 ? -1 : r.hit.mat;
+    }
+    return RT_OK;
+}
+int32_t oracle_occluded_rays(void* scene, int32_t n, const double* o, const double* d, const double* tmax,
+                             const double* time, uint8_t* out) {
+    using namespace orc;
+    const Context& C = static_cast<OracleScene*>(scene)->C;
+    Counters k;
+    for (int32_t i = 0; i < n; ++i) {
+        Ray r(v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]), time[i]);
+        r.tMax = tmax[i];
+        out[i] = (C.hasTlas && occludedTLAS(C, r, C.intersectionTestEpsilon, k)) ? 1 : 0;
+    }
+    return RT_OK;
+}
+
 }  // extern "C"

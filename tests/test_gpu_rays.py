@@ -1,0 +1,130 @@
+"""Traversal parity on explicit rays (rt_debug_trace_rays / rt_debug_occluded_rays vs the
+oracle's intersectTLAS / occludedTLAS, RTContext.swift:619-781).
+
+Camera rays almost never have a zero direction component, so the frame tests exercise the
+`FAST` slab only.  These rays are built to hit the exact-semantics paths and the tie rules:
+axis-aligned and signed-zero directions (1/d = +-inf, NaN slab products), rays
+through shared vertices and edges of a grid (equal-t triangles: first visited wins, H2),
+grazing rays along box faces, and rays mixed in one wave with ordinary ones.  Hits must be
+bit-identical: t, world point, world normal and material."""
+import numpy as np
+import pytest
+
+import myraytracer_amd as M
+from myraytracer_amd import scenes
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _axis_dirs():
+    d = []
+    for a in range(3):
+        for s in (1.0, -1.0):
+            v = [0.0, 0.0, 0.0]; v[a] = s; d.append(v)
+    for a in range(3):                                   # one zero component, incl. -0.0
+        for z in (0.0, -0.0):
+            v = [0.6, -0.8, 0.3]; v[a] = z
+            d.append(list(np.asarray(v) / np.linalg.norm(v)))
+    return np.array(d)
+
+
+def _ray_set(center, radius, n_random, seed):
+    rng = np.random.RandomState(seed)
+    o = center + rng.uniform(-radius, radius, size=(n_random, 3))
+    d = rng.normal(size=(n_random, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    ax = _axis_dirs()
+    oa = np.repeat(center[None, :] + rng.uniform(-0.3 * radius, 0.3 * radius, size=(len(ax), 3)), 1, axis=0)
+    # interleave so axis-aligned rays share waves with ordinary ones
+    O = np.concatenate([o[: n_random // 2], oa, o[n_random // 2:], oa + 0.25 * radius])
+    D = np.concatenate([d[: n_random // 2], ax, d[n_random // 2:], -ax])
+    return O, D
+
+
+def _check_closest(sc, O, D, tmin=None, time=None):
+    eng = M.RayTracerEngine(sc)
+    tg, pg, ng, mg = eng.trace_rays(O, D, tmin, time)
+    to, po, no, mo = oracle.OracleScene(sc).trace_rays(O, D, tmin, time)
+    eng.close()
+    hit = np.isfinite(to)
+    assert np.array_equal(tg, to), f"t differs on {int((tg != to).sum())} of {len(to)} rays"
+    assert np.array_equal(mg, mo)
+    assert np.array_equal(pg[hit], po[hit]) and np.array_equal(ng[hit], no[hit])
+    return hit
+
+
+def _check_occluded(sc, O, D, tmax, time=None):
+    eng = M.RayTracerEngine(sc)
+    g = eng.occluded_rays(O, D, tmax, time)
+    o = oracle.OracleScene(sc).occluded_rays(O, D, tmax, time)
+    eng.close()
+    assert np.array_equal(g, o), f"occlusion differs on {int((g != o).sum())} rays"
+    return o
+
+
+@pytest.mark.parametrize("walk", ["unified", "general"])
+def test_c2_random_and_axis_rays(walk, monkeypatch):
+    monkeypatch.setenv("MYRT_UNIFIED", "1" if walk == "unified" else "0")
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
+    O, D = _ray_set(np.array([0.0, 0.0, 0.0]), 2.5, 4000, 7)
+    hit = _check_closest(sc, O, D)
+    assert 0.2 < hit.mean() < 0.95
+    tmax = np.random.RandomState(3).uniform(0.05, 4.0, size=len(O))
+    occ = _check_occluded(sc, O, D, tmax)
+    assert 0.05 < occ.mean() < 0.95
+
+
+def test_grid_vertices_edges_and_faces():
+    """Vertical rays through heightfield grid vertices, edge midpoints and cell centres:
+    1/d has +-inf components and several triangles share the exact hit."""
+    hp, hf = scenes.heightfield(64, 20.0, 2.0, 5)
+    hp32 = hp.astype(np.float32).astype(np.float64)
+    mesh = M.Mesh(id=1, material="1", positions=hp32, indices=hf.astype(np.int32), indices_one_based=False,
+                  shading_mode="flat")
+    sc = scenes.scaled(scenes.scene_c1(8, 8), 8, 8)
+    sc.objects = [mesh]
+    rng = np.random.RandomState(11)
+    verts = hp32[rng.choice(len(hp32), 300, replace=False)]
+    tri = hf[rng.choice(len(hf), 300, replace=False)]
+    a, b, c = hp32[tri[:, 0]], hp32[tri[:, 1]], hp32[tri[:, 2]]
+    pts = np.concatenate([verts, 0.5 * (a + b), 0.5 * (b + c), (a + b + c) / 3.0])
+    O = pts + np.array([0.0, 10.0, 0.0])
+    D = np.tile([0.0, -1.0, 0.0], (len(O), 1))
+    hit = _check_closest(sc, O, D)
+    # MT is not watertight: exactly on shared vertices/edges both triangles can reject the
+    # ray (u, v rounding), in the reference as here; the centroids always hit
+    assert hit[-300:].all() and hit.mean() > 0.25
+    # grazing: rays in the plane of the grid's bounding faces, along +x and -z
+    lo, hi = hp32.min(0), hp32.max(0)
+    ys = np.linspace(lo[1], hi[1], 40)
+    Og = np.concatenate([np.stack([np.full(40, lo[0] - 1), ys, np.full(40, lo[2])], 1),
+                         np.stack([np.full(40, hi[0]), ys, np.full(40, hi[2] + 1)], 1)])
+    Dg = np.concatenate([np.tile([1.0, 0.0, 0.0], (40, 1)), np.tile([0.0, 0.0, -1.0], (40, 1))])
+    _check_closest(sc, Og, Dg)
+    _check_occluded(sc, O, D, np.full(len(O), 9.999))
+
+
+def test_instances_transforms_and_primitives():
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
+    base = sc.objects[0]
+    sc.objects = [base,
+                  M.MeshInstance(id=11, base_mesh_id=base.id, material="1",
+                                 transform=(2, 0, 0, 0, 0, 2, 0, 0, 0, 0, 2, 0, 3.0, 0.5, -2.0, 1)),
+                  M.Sphere(center=(-2.5, 0.3, 0.5), radius=0.7, material="1"),
+                  M.Plane(center=(0.0, -1.5, 0.0), normal=(0.0, 1.0, 0.0), material="1"),
+                  M.Triangle(vertices=((-3, -1, -3), (3, -1, -3), (0, 2, -3.5)), material="1")]
+    O, D = _ray_set(np.array([0.5, 0.0, 0.0]), 4.0, 3000, 21)
+    _check_closest(sc, O, D)
+    _check_occluded(sc, O, D, np.random.RandomState(5).uniform(0.1, 6.0, size=len(O)))
+
+
+def test_motion_blur_times_and_tmin():
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
+    base = sc.objects[0]
+    base.motion_blur = (0.0, 0.2, 0.0)
+    sc.objects = [base, M.MeshInstance(id=21, base_mesh_id=base.id, material="1",
+                                       transform=M.translation(0.5, 0.0, 0.5), motion_blur=(0.3, 0.0, 0.0))]
+    O, D = _ray_set(np.array([0.0, 0.0, 0.0]), 2.5, 2000, 9)
+    rng = np.random.RandomState(2)
+    _check_closest(sc, O, D, tmin=rng.uniform(0.0, 0.5, size=len(O)), time=rng.uniform(0, 1, size=len(O)))
