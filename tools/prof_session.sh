@@ -3,7 +3,7 @@
 # usage: tools/prof_session.sh TAG [extra bench args...]
 set -u
 tag="$1"; shift
-B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline $*"
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path $*"
 exec_steps=(
   "${tag}_trace|400|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_trace -- $B"
   "${tag}_fetch|400|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_fetch -- $B"
