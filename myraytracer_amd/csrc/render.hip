@@ -372,15 +372,35 @@ static void free_replica(DeviceReplica& r) {
     r = DeviceReplica();
 }
 
-static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r) {
+// Replica from another replica's device buffers: device-to-device over xGMI (or a local
+// copy when both live on one GPU) instead of a second PCIe upload from the host.
+template <class T>
+static int32_t replicate(const std::vector<T>& v, const T* src, int src_dev, T** dst, int dst_dev, int64_t& bytes) {
+    const size_t n = std::max<size_t>(1, v.size());
+    HIP_TRY(hipMalloc((void**)dst, n * sizeof(T)));
+    if (!v.empty()) HIP_TRY(hipMemcpyPeer(*dst, dst_dev, src, src_dev, v.size() * sizeof(T)));
+    bytes += (int64_t)(n * sizeof(T));
+    return RT_OK;
+}
+
+static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, const DeviceReplica* src = nullptr) {
     r.device = device;
     HIP_TRY(hipSetDevice(device));
     int32_t rc;
-    if ((rc = upload(S.recs, &r.recs, r.bytes)) != RT_OK) return rc;
-    if ((rc = upload(S.crecs, &r.crecs, r.bytes)) != RT_OK) return rc;
-    if ((rc = upload(S.ctris, &r.ctris, r.bytes)) != RT_OK) return rc;
-    if ((rc = upload(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
-    if ((rc = upload(S.normals, &r.normals, r.bytes)) != RT_OK) return rc;
+    if (src) {   // the bulk arrays (records, triangles, normals) come from `src` over the fabric
+        const int sd = src->device;
+        if ((rc = replicate(S.recs, src->recs, sd, &r.recs, device, r.bytes)) != RT_OK) return rc;
+        if ((rc = replicate(S.crecs, src->crecs, sd, &r.crecs, device, r.bytes)) != RT_OK) return rc;
+        if ((rc = replicate(S.ctris, src->ctris, sd, &r.ctris, device, r.bytes)) != RT_OK) return rc;
+        if ((rc = replicate(S.tris, src->tris, sd, &r.tris, device, r.bytes)) != RT_OK) return rc;
+        if ((rc = replicate(S.normals, src->normals, sd, &r.normals, device, r.bytes)) != RT_OK) return rc;
+    } else {
+        if ((rc = upload(S.recs, &r.recs, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload(S.crecs, &r.crecs, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload(S.ctris, &r.ctris, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload(S.normals, &r.normals, r.bytes)) != RT_OK) return rc;
+    }
     if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.tlas_leaf, &r.tlas_leaf, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.mats, &r.mats, r.bytes)) != RT_OK) return rc;
@@ -599,7 +619,20 @@ int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32
         auto t0 = std::chrono::steady_clock::now();
         s->devs.resize(devs.size());
         for (size_t k = 0; k < devs.size(); ++k) {
-            rc = make_replica(s->host, devs[k], s->devs[k]);
+            // replicas after the first copy from replica 0 when the fabric allows it
+            const DeviceReplica* src = nullptr;
+            if (k > 0) {
+                int can = (devs[k] == devs[0]) ? 1 : 0;
+                if (!can && hipDeviceCanAccessPeer(&can, devs[k], devs[0]) != hipSuccess) can = 0;
+                if (can && devs[k] != devs[0]) {
+                    (void)hipSetDevice(devs[k]);
+                    const hipError_t pe = hipDeviceEnablePeerAccess(devs[0], 0);
+                    if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) can = 0;
+                    (void)hipGetLastError();
+                }
+                if (can) src = &s->devs[0];
+            }
+            rc = make_replica(s->host, devs[k], s->devs[k], src);
             if (rc != RT_OK) {
                 std::string e = g_err;
                 for (auto& r : s->devs) free_replica(r);

@@ -3,6 +3,8 @@ spheres and planes (RTContext.swift:122-192, 513-538, 851-870), dielectric mater
 two child rays per bounce and Beer absorption (Object+Extension.swift:207-251), and area
 lights with the chunk-sequential jitterIndex (:145-186, :288).  Same bar as
 test_gpu_parity.py: per-channel L-inf <= 1e-5, exact RGBA8, equal ray counts."""
+import copy
+
 import numpy as np
 import pytest
 
@@ -148,3 +150,17 @@ def test_progress_per_batch_and_cancel():
     assert e.value.code == -60 and len(calls) == 1
     again = eng.render(0)                                            # the engine stays usable
     assert np.array_equal(again.rgb, r.rgb)
+
+
+def test_second_camera_and_empty_selection():
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 96, 64)
+    c2 = copy.deepcopy(sc.cameras[0])
+    c2.position = (1.5, 1.0, 3.5)
+    c2.image_resolution = (72, 40)                                   # 5 chunks
+    sc.cameras.append(c2)
+    eng = M.RayTracerEngine(sc)
+    rgb, rgba, st = eng.render_rows(1, 0, 1, True)
+    ref, ref8, _ = oracle.OracleScene(sc).render(1, threads=0, rgba=True)
+    assert rgb.shape == (40, 72, 3) and float(np.abs(rgb - ref).max()) <= TOL and np.array_equal(rgba, ref8)
+    empty, _, st0 = eng.render_rows(1, 7, 1, True)                   # chunk 7 is past the image
+    assert empty.shape == (0, 72, 3) and st0.primary_rays == 0
