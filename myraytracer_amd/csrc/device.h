@@ -140,6 +140,19 @@ struct Stack {
         }
         ++sp;
     }
+    // push when `keep`; the LDS store is issued regardless (slot sp is free), only the
+    // rare spill store is conditional
+    __device__ __forceinline__ void push_if(bool keep, int ref, double t) {
+        const unsigned long long e = (unsigned long long)(unsigned)ref |
+                                     ((unsigned long long)(unsigned)__double2hiint(t) << 32);
+        if (sp < kLds) {
+            lds[sp * stride] = e;
+        } else if (keep) {
+            asm volatile("" ::: "memory");
+            spill[sp - kLds] = e;
+        }
+        sp += keep ? 1 : 0;
+    }
     // returns the ref; `tlo` = lower bound of the entry distance
     __device__ __forceinline__ int pop(double& tlo) {
         --sp;
@@ -337,15 +350,13 @@ __device__ __forceinline__ bool inner_step_rec(const RenderParams& P, const Rec&
             return false;
         }
     }
-    if (h0 && h1) {
-        const bool sw = t0 > t1;
-        st.push(sw ? a : b, sw ? t0 : t1);
-        ref = sw ? b : a;
-        return true;
-    }
-    if (h0) { ref = a; return true; }
-    if (h1) { ref = b; return true; }
-    return false;
+    // selects instead of branches: the far child's entry is written to the next LDS slot
+    // unconditionally and kept only when both children are hit
+    const bool both = h0 && h1;
+    const bool sw = t0 > t1;
+    st.push_if(both, sw ? a : b, sw ? t0 : t1);
+    ref = both ? (sw ? b : a) : (h0 ? a : b);
+    return h0 || h1;
 }
 
 // A record held in SGPRs: loaded with scalar loads when every active lane of the wave is
