@@ -9,9 +9,11 @@ the reference's `RayTracerEngine` API.
 """
 from .scene import (AreaLight, Camera, Material, Mesh, MeshInstance, Plane, PointLight, Scene, Sphere,  # noqa: F401
                     Triangle, translation)
+from .sceneio import SceneLoadError, load as load_scene, loads as loads_scene, save_png  # noqa: F401
 from .engine import (CameraSpec, RayTracerEngine, RenderError, RenderProgress, RenderResult,  # noqa: F401
                      RenderStats, SceneInfo, load_library, ply_load, rows_for_chunks)
 
 __all__ = ["RayTracerEngine", "Scene", "Camera", "Material", "Mesh", "MeshInstance", "Triangle", "Sphere", "Plane",
            "PointLight", "AreaLight", "RenderResult", "RenderStats", "RenderProgress", "RenderError", "SceneInfo",
-           "CameraSpec", "load_library", "ply_load", "rows_for_chunks", "translation"]
+           "CameraSpec", "load_library", "ply_load", "rows_for_chunks", "translation", "load_scene", "loads_scene",
+           "save_png", "SceneLoadError"]

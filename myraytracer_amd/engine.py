@@ -118,6 +118,19 @@ class RayTracerEngine:
         self._h = handle
         self.devices = devs
 
+    @classmethod
+    def from_file(cls, path, format: str = "auto", devices: Optional[Sequence[int]] = None) -> "RayTracerEngine":
+        """RayTracerEngine.init(from: url) (RayTracer.swift:30-34): JSON or XML scene file."""
+        from . import sceneio
+        return cls(sceneio.load(path, format), devices)
+
+    @classmethod
+    def from_data(cls, data, format: str = "auto", devices: Optional[Sequence[int]] = None,
+                  base_dir: Optional[str] = None) -> "RayTracerEngine":
+        """RayTracerEngine.init(data:) (RayTracer.swift:35-36)."""
+        from . import sceneio
+        return cls(sceneio.loads(data, format, base_dir), devices)
+
     # -- lifecycle
     def close(self):
         if getattr(self, "_h", None):
@@ -194,6 +207,14 @@ class RayTracerEngine:
         rgb, rgba, stats = self.render_rows(camera_index, 0, 1, True, progress)
         spec = self.camera_spec(camera_index)
         return RenderResult(self.scene.cameras[camera_index].image_name, rgba, rgb, spec, stats)
+
+    def save_png(self, path: str, camera_index: int = 0,
+                 progress: Optional[Callable[[RenderProgress], bool]] = None) -> RenderResult:
+        """renderCGImage + ImageHelper.savePNG (RayTracer.swift:105-112, Helpers/Image.swift:14-42)."""
+        from . import sceneio
+        res = self.render(camera_index, progress)
+        sceneio.save_png(res.rgba8, path)
+        return res
 
     def render_all(self, progress: Optional[Callable[[RenderProgress], bool]] = None) -> List[RenderResult]:
         """renderAll (RayTracer.swift:70-102)."""

@@ -149,6 +149,7 @@ class Scene:
     shadow_ray_epsilon: float = 1e-3
     intersection_test_epsilon: float = 1e-6
     max_recursion_depth: int = 6
+    path: Optional[str] = None           # directory of the scene file (Scene.path, RayTracer.swift:34)
 
     # ------------------------------------------------------------------ packing
     def to_desc(self) -> "PackedScene":
