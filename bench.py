@@ -190,6 +190,16 @@ def main():
             ms_h = (time.perf_counter() - t_h) * 1e3 / nh
             host_path = {"ms_per_frame": round(ms_h, 4), "value": round(rays_rank / (ms_h * 1e-3) / 1e6, 2),
                          "unit": "Mrays/s", "what": "rt_render wall time incl. D2H of the FP64 RGB framebuffer"}
+            # caller buffer in page-locked memory (rt_host_alloc): rows DMA'd straight into it
+            pin_rgb, _ = eng.alloc_frame(0, first, step, rgba=False)
+            eng.render_rows(0, first, step, False, out=pin_rgb)
+            t_h = time.perf_counter()
+            for _ in range(nh):
+                eng.render_rows(0, first, step, False, out=pin_rgb)
+            ms_p = (time.perf_counter() - t_h) * 1e3 / nh
+            host_path["pinned"] = {"ms_per_frame": round(ms_p, 4), "value": round(rays_rank / (ms_p * 1e-3) / 1e6, 2),
+                                   "what": "same into a page-locked caller buffer (rt_host_alloc): the kernel stores rows into it over PCIe, no copy"}
+            del pin_rgb
         except Exception as e:  # pragma: no cover
             log("host path failed:", e)
 

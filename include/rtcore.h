@@ -184,6 +184,13 @@ int32_t rt_render(rt_scene* scene, int32_t camera_index, int32_t chunk_first, in
                   double* out_rgb, uint8_t* out_rgba8, rt_stats* stats,
                   rt_progress_fn progress, void* user);
 
+/* Page-locked host buffers for rt_render outputs (hipHostMalloc).  When out_rgb /
+ * out_rgba8 lie inside one such allocation (or in memory the caller registered with
+ * hipHostRegister), rt_render DMAs finished rows straight into them instead of going
+ * through its own pinned staging and a host memcpy.  Any other host memory still works. */
+int32_t rt_host_alloc(uint64_t bytes, void** out);
+void    rt_host_free(void* ptr);
+
 /* Same as rt_render on ONE device slot, but outputs are DEVICE pointers on that
  * device and the work is enqueued on `stream` (a hipStream_t, NULL = default)
  * without host synchronisation.  Ray counters (if stats != NULL) are only valid

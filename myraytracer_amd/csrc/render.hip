@@ -734,6 +734,48 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
     return RT_OK;
 }
 
+// True when [p, p+bytes) lies inside ONE page-locked host allocation (hipHostMalloc /
+// hipHostRegister): the DMA engine can then write it directly.  NULL counts as true.
+static int32_t env_int(const char* name, int32_t def, int32_t lo, int32_t hi) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return def;
+    return std::min(hi, std::max(lo, (int32_t)std::atoi(v)));
+}
+
+static bool pinned_range(const void* p, size_t bytes) {
+    if (!p || bytes == 0) return true;
+    const void* ends[2] = {p, static_cast<const char*>(p) + bytes - 1};
+    unsigned long long id[2] = {0, 0};
+    for (int k = 0; k < 2; ++k) {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, ends[k]) != hipSuccess) { (void)hipGetLastError(); return false; }
+        if (a.type != hipMemoryTypeHost) return false;
+        if (hipPointerGetAttribute(&id[k], HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                                   reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(ends[k]))) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+    }
+    return id[0] == id[1];
+}
+
+int32_t rt_host_alloc(uint64_t bytes, void** out) {
+    if (!out) return fail(RT_ERR_INVALID_ARG, "null output pointer");
+    *out = nullptr;
+    if (bytes == 0) return RT_OK;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        return fail(RT_ERR_OOM, "hipHostMalloc failed");
+    }
+    return RT_OK;
+}
+
+void rt_host_free(void* ptr) {
+    if (ptr) (void)hipHostFree(ptr);
+}
+
+
 // Host-buffer render across all device replicas (Renderer.render + renderRGBA8Async,
 // Object+Extension.swift:52-379, RayTracer.swift:137-205).  Chunk k of the selection goes to
 // replica (k mod D).  Each replica renders its chunks in up to kRenderBatches launches on its
@@ -758,6 +800,22 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
     std::vector<int32_t> rowOff(sel.size() + 1, 0);
     for (size_t q = 0; q < sel.size(); ++q) rowOff[q + 1] = rowOff[q] + std::min(8, H - 8 * sel[q]);
     const int32_t rowsTotal = rowOff.back();
+    // outputs in page-locked memory: finished rows are DMA'd straight into the caller's
+    // buffer (coalesced per run of adjacent chunks) and the host scatter disappears
+    const bool direct = pinned_range(out_rgb, (size_t)rowsTotal * W * 3 * sizeof(double)) &&
+                        pinned_range(out_rgba8, (size_t)rowsTotal * W * 4);
+    // one replica writing a pinned caller buffer: the kernels store rows straight into it
+    // over PCIe (host-mapped) while they render, with no copy at all
+    double* zc_rgb = nullptr; uint8_t* zc_rgba = nullptr;
+    const bool zerocopy = direct && D == 1 && env_int("MYRT_ZEROCOPY", 1, 0, 1) == 1 &&
+        (!out_rgb || hipHostGetDevicePointer((void**)&zc_rgb, out_rgb, 0) == hipSuccess) &&
+        (!out_rgba8 || hipHostGetDevicePointer((void**)&zc_rgba, out_rgba8, 0) == hipSuccess);
+    (void)hipGetLastError();
+    // Launches per replica.  Each batch ends on its slowest tile, so batches cost time
+    // (~0.1-0.2 ms each on C3): they are used for progress granularity when a callback is
+    // given, and otherwise only to overlap the copy of batch b with the render of b+1.
+    const int32_t nBatches = env_int("MYRT_BATCHES", progress ? kRenderBatches : (zerocopy ? 1 : 2),
+                                     1, kRenderBatches);
 
     // ---- per replica: its chunk list, batch plan, buffers; enqueue everything
     struct Plan { int32_t myFirst, myStep, nChunks, rows, nb, per; std::vector<int32_t> batchRow; };
@@ -770,7 +828,7 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
         for (int32_t c = pl.myFirst; c < num_chunks_total(H); c += pl.myStep) pl.nChunks++;
         pl.rows = rt_rows_for_chunks(H, pl.myFirst, pl.myStep);
         if (pl.nChunks == 0) { pl.nb = 0; continue; }
-        pl.per = (pl.nChunks + kRenderBatches - 1) / kRenderBatches;
+        pl.per = (pl.nChunks + nBatches - 1) / nBatches;
         pl.nb = (pl.nChunks + pl.per - 1) / pl.per;
         pl.batchRow.assign(pl.nb + 1, 0);
         for (int32_t b = 0; b < pl.nb; ++b) {
@@ -810,20 +868,52 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
             HIP_TRY(hipSetDevice(r.device));
             const int32_t c0 = pl.myFirst + b * pl.per * pl.myStep;
             const int32_t nc = std::min(pl.per, pl.nChunks - b * pl.per);
-            double* drgb = r.out_d + (size_t)pl.batchRow[b] * W * 3;
-            uint8_t* drgba = out_rgba8 ? r.out8_d + (size_t)pl.batchRow[b] * W * 4 : nullptr;
+            double* drgb = (zerocopy && zc_rgb ? zc_rgb : r.out_d) + (size_t)pl.batchRow[b] * W * 3;
+            uint8_t* drgba = out_rgba8 ? (zerocopy ? zc_rgba : r.out8_d) + (size_t)pl.batchRow[b] * W * 4 : nullptr;
             RenderParams P = make_params(s, r, cam, c0, pl.myStep, drgb, drgba);
             P.num_chunks = nc;
             const int32_t lrc = launch(s, r, P, r.stream, false);
             if (lrc != RT_OK) return lrc;
             HIP_TRY(hipEventRecord(r.batch_done[b], r.stream));
             const size_t nrows = (size_t)(pl.batchRow[b + 1] - pl.batchRow[b]);
+            if (zerocopy) {                                  // rows already in the caller's buffer
+                HIP_TRY(hipEventRecord(r.batch_copied[b], r.stream));
+                continue;
+            }
             HIP_TRY(hipStreamWaitEvent(r.copy_stream, r.batch_done[b], 0));
-            HIP_TRY(hipMemcpyAsync(r.host_rgb + (size_t)pl.batchRow[b] * W * 3, drgb, nrows * W * 3 * sizeof(double),
-                                   hipMemcpyDeviceToHost, r.copy_stream));
-            if (out_rgba8)
-                HIP_TRY(hipMemcpyAsync(r.host_rgba + (size_t)pl.batchRow[b] * W * 4, drgba, nrows * W * 4,
-                                       hipMemcpyDeviceToHost, r.copy_stream));
+            if (direct) {
+                // replica k's q-th chunk is selection entry k + q*D; its rows follow the
+                // batch's earlier chunks in drgb
+                int32_t q = b * pl.per;
+                const int32_t qEnd = q + nc;
+                size_t srcRow = 0;
+                while (q < qEnd) {
+                    const size_t e0 = (size_t)k + (size_t)q * D;
+                    int32_t nr = rowOff[e0 + 1] - rowOff[e0];
+                    int32_t q1 = q + 1;
+                    while (q1 < qEnd) {                     // extend over adjacent output rows
+                        const size_t e = (size_t)k + (size_t)q1 * D;
+                        if (rowOff[e] != rowOff[e0] + nr) break;
+                        nr += rowOff[e + 1] - rowOff[e];
+                        ++q1;
+                    }
+                    if (out_rgb)
+                        HIP_TRY(hipMemcpyAsync(out_rgb + (size_t)rowOff[e0] * W * 3, drgb + srcRow * W * 3,
+                                               (size_t)nr * W * 3 * sizeof(double), hipMemcpyDeviceToHost,
+                                               r.copy_stream));
+                    if (out_rgba8)
+                        HIP_TRY(hipMemcpyAsync(out_rgba8 + (size_t)rowOff[e0] * W * 4, drgba + srcRow * W * 4,
+                                               (size_t)nr * W * 4, hipMemcpyDeviceToHost, r.copy_stream));
+                    srcRow += (size_t)nr;
+                    q = q1;
+                }
+            } else {
+                HIP_TRY(hipMemcpyAsync(r.host_rgb + (size_t)pl.batchRow[b] * W * 3, drgb,
+                                       nrows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, r.copy_stream));
+                if (out_rgba8)
+                    HIP_TRY(hipMemcpyAsync(r.host_rgba + (size_t)pl.batchRow[b] * W * 4, drgba, nrows * W * 4,
+                                           hipMemcpyDeviceToHost, r.copy_stream));
+            }
             HIP_TRY(hipEventRecord(r.batch_copied[b], r.copy_stream));
         }
         return RT_OK;
@@ -845,6 +935,11 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
             HIP_TRY(hipSetDevice(r.device));
             HIP_TRY(hipEventSynchronize(r.batch_copied[b]));
             if (cancelled) continue;
+            if (direct) {
+                rowsDone += pl.batchRow[b + 1] - pl.batchRow[b];
+                if (progress && !progress(user, rowsDone, rowsTotal)) cancelled = true;
+                continue;
+            }
             // replica k's q-th chunk is selection entry k + q*D; chunks are scattered by
             // several threads (host memcpy bandwidth, not PCIe, bounds this step)
             const int32_t q0 = b * pl.per, q1 = std::min(pl.nChunks, q0 + pl.per);

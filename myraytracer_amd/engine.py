@@ -169,11 +169,21 @@ class RayTracerEngine:
                          int(i.meshes), int(i.triangles), int(i.spheres), int(i.planes))
 
     # -- rendering
+    def alloc_frame(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1, rgba: bool = True):
+        """Page-locked (rgb, rgba) output arrays for a chunk selection (rt_host_alloc): passed to
+        render_rows as out/out_rgba, finished rows are DMA'd into them with no host copy."""
+        cam = self.scene.cameras[camera_index]
+        W, H = max(1, int(cam.image_resolution[0])), max(1, int(cam.image_resolution[1]))
+        rows = load_library().rt_rows_for_chunks(H, chunk_first, chunk_step)
+        rgb = pinned_array((rows, W, 3), np.float64)
+        return rgb, (pinned_array((rows, W, 4), np.uint8) if rgba else None)
+
     def render_rows(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
                     want_rgba: bool = True, progress: Optional[Callable[[RenderProgress], bool]] = None,
-                    out: Optional[np.ndarray] = None):
+                    out: Optional[np.ndarray] = None, out_rgba: Optional[np.ndarray] = None):
         """Render the selected 8-row chunks; returns (rgb[rows,W,3] f64, rgba[rows,W,4] u8, RenderStats).
-        `out`: optional reusable C-contiguous float64 (rows, W, 3) array for the RGB result."""
+        `out` / `out_rgba`: optional reusable C-contiguous (rows, W, 3) float64 / (rows, W, 4) uint8
+        arrays for the results (page-locked ones from alloc_frame take the direct-DMA path)."""
         lib = load_library()
         if not (0 <= camera_index < len(self.scene.cameras)):
             raise RenderError(A.RT_ERR_INVALID_CAMERA, "Invalid camera index")
@@ -184,7 +194,13 @@ class RayTracerEngine:
             rgb = out
         else:
             rgb = np.empty((rows, W, 3), dtype=np.float64)
-        rgba = np.empty((rows, W, 4), dtype=np.uint8) if want_rgba else None
+        if not want_rgba:
+            rgba = None
+        elif out_rgba is not None and out_rgba.shape == (rows, W, 4) and out_rgba.dtype == np.uint8 \
+                and out_rgba.flags.c_contiguous:
+            rgba = out_rgba
+        else:
+            rgba = np.empty((rows, W, 4), dtype=np.uint8)
         st = A.rt_stats()
 
         def _cb(user, done, total):
@@ -192,7 +208,7 @@ class RayTracerEngine:
                 return 1
             return 1 if progress(RenderProgress(done / max(total, 1), f"Row {done}/{total}")) else 0
 
-        cb = A.RT_PROGRESS_FN(_cb)
+        cb = A.RT_PROGRESS_FN(_cb) if progress is not None else A.RT_PROGRESS_FN()
         _check(lib.rt_render(self._h, camera_index, chunk_first, chunk_step,
                              rgb.ctypes.data_as(A.c_double_p),
                              rgba.ctypes.data_as(C.POINTER(C.c_uint8)) if rgba is not None else None,
@@ -274,6 +290,22 @@ def _ray_arrays(origins, dirs, tlim, time):
     tl = np.zeros(n) if tlim is None else np.ascontiguousarray(np.broadcast_to(tlim, (n,)), dtype=np.float64)
     tm = np.zeros(n) if time is None else np.ascontiguousarray(np.broadcast_to(time, (n,)), dtype=np.float64)
     return o, d, n, tl, tm
+
+
+def pinned_array(shape, dtype) -> np.ndarray:
+    """numpy array over page-locked host memory (rt_host_alloc); freed with the array."""
+    import weakref
+    lib = load_library()
+    dt = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dt.itemsize
+    if nbytes == 0:
+        return np.empty(shape, dt)
+    p = C.c_void_p()
+    _check(lib.rt_host_alloc(nbytes, C.byref(p)))
+    buf = (C.c_uint8 * nbytes).from_address(p.value)
+    arr = np.frombuffer(buf, dtype=dt).reshape(shape)
+    weakref.finalize(buf, lib.rt_host_free, C.c_void_p(p.value))
+    return arr
 
 
 def rows_for_chunks(height: int, chunk_first: int, chunk_step: int) -> int:

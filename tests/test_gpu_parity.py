@@ -162,6 +162,28 @@ def test_two_replicas_gather_matches_single():
     assert one.stats.shadow_rays == two.stats.shadow_rays
 
 
+@pytest.mark.parametrize("devices,first,step", [([0], 0, 1), ([0], 1, 3), ([0, 0], 0, 1), ([0, 0, 0], 2, 2)])
+def test_pinned_outputs_take_direct_dma(devices, first, step):
+    """rt_render into page-locked caller buffers (rt_host_alloc): rows are DMA'd straight into
+    them, coalesced per run of adjacent chunks; results equal the pageable (staged) path."""
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 136, 100)  # 13 chunks, last partial
+    eng = M.RayTracerEngine(sc, devices=devices)
+    rgb_p, rgba_p, st_p = eng.render_rows(0, first, step, True)
+    prgb, prgba = eng.alloc_frame(0, first, step)
+    prgb.fill(-1.0)
+    prgba.fill(7)
+    rgb_d, rgba_d, st_d = eng.render_rows(0, first, step, True, out=prgb, out_rgba=prgba)
+    assert rgb_d is prgb and rgba_d is prgba
+    assert np.array_equal(rgb_d, rgb_p) and np.array_equal(rgba_d, rgba_p)
+    assert (st_d.primary_rays, st_d.shadow_rays) == (st_p.primary_rays, st_p.shadow_rays)
+    # RGB only, then progress reaches the total
+    seen = []
+    prgb.fill(-1.0)
+    eng.render_rows(0, first, step, False, progress=lambda p: seen.append(p.fraction) or True, out=prgb)
+    assert np.array_equal(prgb, rgb_p) and seen and seen[-1] == 1.0
+    eng.close()
+
+
 def test_device_path_matches_host_path():
     import torch
     sc = scenes.scaled(scenes.scene_c2(inline=True), 200, 120)
