@@ -62,10 +62,26 @@ def build_ref(force: bool = False) -> str:
     return out
 
 
+def build_cpp_tests(force: bool = False) -> str:
+    """tests/cpp/engine_test: the C++ host (include/rt_engine.hpp) driving libmyrt.so, checked
+    against the oracle (test infrastructure; run by tests/test_cpp_host.py)."""
+    src = os.path.join(ROOT, "tests", "cpp", "engine_test.cpp")
+    out = os.path.join(ROOT, "tests", "cpp", "engine_test")
+    deps = [src, os.path.join(ROOT, "include", "rt_engine.hpp"), os.path.join(ROOT, "include", "rtcore.h"),
+            os.path.join(PKG, "libmyrt.so"), os.path.join(ROOT, "oracle", "liboracle.so")]
+    if force or _stale(out, deps):
+        _run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"), "-o", out, src,
+              "-L", PKG, "-lmyrt", "-L", os.path.join(ROOT, "oracle"), "-loracle", "-L/opt/rocm/lib",
+              "-Wl,-rpath,$ORIGIN/../../myraytracer_amd", "-Wl,-rpath,$ORIGIN/../../oracle",
+              "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
+    return out
+
+
 def build_all(force: bool = False):
     build_product(force)
     build_oracle(force)
     build_ref(force)
+    build_cpp_tests(force)
 
 
 if __name__ == "__main__":

@@ -19,6 +19,7 @@ def _built():
     from myraytracer_amd import build as B
     B.build_product()
     B.build_oracle()
+    B.build_cpp_tests()
     yield
 
 
