@@ -112,7 +112,7 @@ EXPORTED_SYMBOLS = [
     "rt_scene_create", "rt_scene_destroy", "rt_scene_info_get", "rt_render", "rt_render_device",
     "rt_stats_collect", "rt_rows_for_chunks", "rt_render_device_counted", "rt_last_error", "rt_version",
     "rt_ply_load", "rt_ply_free", "rt_debug_bvh_hash", "rt_debug_host_build",
-    "rt_debug_trace_rays", "rt_debug_occluded_rays", "rt_host_alloc", "rt_host_free",
+    "rt_debug_trace_rays", "rt_debug_occluded_rays", "rt_host_alloc", "rt_host_free", "rt_debug_wave_times",
 ]
 
 
@@ -150,6 +150,9 @@ def bind(lib: C.CDLL) -> C.CDLL:
     lib.rt_host_alloc.restype = C.c_int32
     lib.rt_host_free.argtypes = [C.c_void_p]
     lib.rt_host_free.restype = None
+    lib.rt_debug_wave_times.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                        P(C.c_uint64), C.c_int64, P(C.c_int64)]
+    lib.rt_debug_wave_times.restype = C.c_int32
     lib.rt_debug_bvh_hash.argtypes = [C.c_void_p, C.c_int32]
     lib.rt_debug_bvh_hash.restype = C.c_uint64
     lib.rt_debug_host_build.argtypes = [P(rt_scene_desc), P(C.c_uint64), C.c_int32, c_int32_p, P(rt_scene_info)]

@@ -434,21 +434,49 @@ __device__ __forceinline__ SCRec load_crec_scalar(const CRec* pv) {
     return R;
 }
 
+#ifndef MYRT_CREC56
+#define MYRT_CREC56 0
+#endif
+// The 56 used bytes of a compact record (3 x dwordx4 + dwordx2; the 8 pad bytes are not
+// fetched): 12.5% less data through the texture-data path per vector record load.
+__device__ __forceinline__ CRec load_crec56(const CRec* p) {
+    const float4* q = reinterpret_cast<const float4*>(p);
+    const float4 a = q[0], b = q[1], e = q[2];
+    const int2 r = *reinterpret_cast<const int2*>(q + 3);
+    CRec R;
+    R.lo[0][0] = a.x; R.lo[0][1] = a.y; R.lo[0][2] = a.z; R.lo[1][0] = a.w;
+    R.lo[1][1] = b.x; R.lo[1][2] = b.y; R.hi[0][0] = b.z; R.hi[0][1] = b.w;
+    R.hi[0][2] = e.x; R.hi[1][0] = e.y; R.hi[1][1] = e.z; R.hi[1][2] = e.w;
+    R.ref[0] = r.x; R.ref[1] = r.y;
+    return R;
+}
+
 // One inner record: compact (float32 bounds, exact) below P.compact_limit, else full;
 // through the scalar cache when the whole wave is at this node.
 template <bool COUNT, bool FAST, bool SHADOW>
 __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
                                            Stack& st, Counts& c) {
     const int r0 = __builtin_amdgcn_readfirstlane(ref);
+#ifndef MYRT_SCALAR_FULL
+#define MYRT_SCALAR_FULL 1
+#endif
     if (P.scalar_nodes && __all(ref == r0)) {
         if (r0 < P.compact_limit) {
             const SCRec R = load_crec_scalar(P.crecs + r0);
             return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
         }
+#if MYRT_SCALAR_FULL
         const SRec R = load_rec_scalar(P.recs + r0);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
+#endif
     }
-    if (ref < P.compact_limit) return inner_step_rec<COUNT, FAST, SHADOW>(P, P.crecs[ref], ref, o, inv, lim, st, c);
+    if (ref < P.compact_limit) {
+#if MYRT_CREC56
+        return inner_step_rec<COUNT, FAST, SHADOW>(P, load_crec56(P.crecs + ref), ref, o, inv, lim, st, c);
+#else
+        return inner_step_rec<COUNT, FAST, SHADOW>(P, P.crecs[ref], ref, o, inv, lim, st, c);
+#endif
+    }
     return inner_step_rec<COUNT, FAST, SHADOW>(P, P.recs[ref], ref, o, inv, lim, st, c);
 }
 
@@ -619,46 +647,104 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
 // (RTContext.swift:648-706).  One call = one step: one inner record or one leaf run,
 // followed by the pop of the next node.  Returns 0 = continue, 1 = stack exhausted,
 // 2 = shadow ray occluded.
+// Leaf of the unified walk: a BLAS leaf run (closest: record hits in h; any-hit: true when
+// occluded) or a TLAS leaf (pushes its instances' BLAS roots in reverse order).
+template <bool COUNT, bool SHADOW, bool FAST>
+__device__ __forceinline__ bool unified_leaf(const RenderParams& P, int ref, Stack& st, const V3& o, const V3& d,
+                                             const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
+    const double eps = P.eps;
+    const int e = ~ref;
+    if (e < P.tlas_leaf_base) {                                  // BLAS leaf run
+        auto run = [&](const auto* tris) -> bool {
+            for (int t = e;; ++t) {
+                const auto& T = tris[t];
+                if (COUNT) c.tris++;
+                if (SHADOW) {
+                    if (tri_shadow(T, o, d, 0.0, tmax, eps)) return true;
+                } else {
+                    tri_closest(T, o, d, tlo, eps, h, t, T.prim); // prim = owning instance
+                }
+                if (T.last) break;
+            }
+            return false;
+        };
+        return P.ctris ? run(P.ctris) : run(P.tris);
+    }
+    // TLAS leaf: instance list
+    const int k0 = e - P.tlas_leaf_base;
+    int k1 = k0;
+    while (!P.tlas_leaf[k1].last) ++k1;
+    const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+    for (int k = k1; k >= k0; --k) {
+        const DInstance& I = P.insts[P.tlas_leaf[k].inst];
+        if (COUNT) c.insts++;
+        double dr;
+        if (slab_hit<FAST>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                           I.root_hi[2], o, inv, eps, dr) && !(dr > lim))
+            st.push(I.root_ref, dr);
+    }
+    return false;
+}
+
+#ifndef MYRT_ONE_TRI
+#define MYRT_ONE_TRI 0
+#endif
 template <bool COUNT, bool SHADOW, bool FAST>
 __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Stack& st, const V3& o, const V3& d,
                                             const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
-    const double eps = P.eps;
     if (ref >= 0) {
         if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c))
             return 0;
-    } else {
-        const int e = ~ref;
-        if (e < P.tlas_leaf_base) {                                  // BLAS leaf run
-            auto run = [&](const auto* tris) -> bool {
-                for (int t = e;; ++t) {
-                    const auto& T = tris[t];
-                    if (COUNT) c.tris++;
-                    if (SHADOW) {
-                        if (tri_shadow(T, o, d, 0.0, tmax, eps)) return true;
-                    } else {
-                        tri_closest(T, o, d, tlo, eps, h, t, T.prim); // prim = owning instance
-                    }
-                    if (T.last) break;
-                }
-                return false;
-            };
-            if (P.ctris ? run(P.ctris) : run(P.tris)) return 2;
-        } else {                                                      // TLAS leaf: instance list
-            const int k0 = e - P.tlas_leaf_base;
-            int k1 = k0;
-            while (!P.tlas_leaf[k1].last) ++k1;
-            const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
-            for (int k = k1; k >= k0; --k) {
-                const DInstance& I = P.insts[P.tlas_leaf[k].inst];
-                if (COUNT) c.insts++;
-                double dr;
-                if (slab_hit<FAST>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
-                                   I.root_hi[2], o, inv, eps, dr) && !(dr > lim))
-                    st.push(I.root_ref, dr);
+    } else if (MYRT_ONE_TRI && ~ref < P.tlas_leaf_base) {
+        // one triangle per iteration: a lane in a 2-triangle leaf continues with the second
+        // triangle next iteration while the other lanes keep traversing, so an iteration
+        // pays for at most one record and one triangle
+        const int t = ~ref;
+        auto one = [&](const auto* tris) -> int {
+            const auto& T = tris[t];
+            if (COUNT) c.tris++;
+            if (SHADOW) {
+                if (tri_shadow(T, o, d, 0.0, tmax, P.eps)) return 2;
+            } else {
+                tri_closest(T, o, d, tlo, P.eps, h, t, T.prim);
             }
-        }
+            return T.last ? 1 : 0;
+        };
+        const int r = P.ctris ? one(P.ctris) : one(P.tris);
+        if (r == 2) return 2;
+        if (r == 0) { ref = ~(t + 1); return 0; }
+    } else {
+        if (unified_leaf<COUNT, SHADOW, FAST>(P, ref, st, o, d, inv, tlo, tmax, h, c)) return 2;
     }
     return pop_next<COUNT, SHADOW>(P, st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref, c) ? 0 : 1;
+}
+
+#ifndef MYRT_WHILE_WHILE
+#define MYRT_WHILE_WHILE 0
+#endif
+// While-while form (Aila & Laine 2009): a lane descends through inner records until it sits
+// at a leaf, and leaves are processed only once every lane of the wave has left the inner
+// loop, so one wave iteration no longer pays for both the record and the triangle path.
+// Returns 1 = stack exhausted, 2 = occluded.  Visit order is unchanged.
+template <bool COUNT, bool SHADOW, bool FAST>
+__device__ __forceinline__ int unified_walk_ww(const RenderParams& P, int ref, Stack& st, const V3& o, const V3& d,
+                                               const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
+    for (;;) {
+        bool alive = true;
+        while (ref >= 0) {
+            if (COUNT) { if (SHADOW) c.it_shadow++; else c.it_closest++; }
+            const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+            if (!inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, lim, st, c) &&
+                !pop_next<COUNT, SHADOW>(P, st, 0, lim, ref, c)) {
+                alive = false;
+                break;
+            }
+        }
+        if (!alive) return 1;
+        if (COUNT) { if (SHADOW) c.it_shadow++; else c.it_closest++; }
+        if (unified_leaf<COUNT, SHADOW, FAST>(P, ref, st, o, d, inv, tlo, tmax, h, c)) return 2;
+        if (!pop_next<COUNT, SHADOW>(P, st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref, c)) return 1;
+    }
 }
 
 // Root test of the unified walk (the TLAS root is popped and tested first,
@@ -678,6 +764,10 @@ __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3
                                                  double tlo, Hit& h, Stack& st, Counts& c) {
     int ref;
     if (!unified_begin(P, o, inv, DINF, ref)) return;   // the stack is empty here (base 0)
+    if (MYRT_WHILE_WHILE) {
+        unified_walk_ww<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c);
+        return;
+    }
     do { if (COUNT) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0);
 }
 template <bool COUNT>
@@ -696,7 +786,11 @@ __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     const int base = st.sp;
     int r;
-    do { if (COUNT) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0);
+    if (MYRT_WHILE_WHILE) {
+        r = unified_walk_ww<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c);
+    } else {
+        do { if (COUNT) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0);
+    }
     st.sp = base;
     return r == 2;
 }

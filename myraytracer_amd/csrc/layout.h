@@ -130,7 +130,7 @@ struct RenderParams {
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
     int32_t scalar_nodes;            // wave-uniform records via scalar loads (device.h inner_step)
     int32_t compact_limit;           // records below this index are read from crecs
-    int32_t pad2;
+    int32_t tile_order;              // megakernel block->tile order: 0 natural, 1 reversed, 2 strided (device.h tile_of)
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)
@@ -140,6 +140,7 @@ struct RenderParams {
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
     unsigned long long* counters;    // [0] shadow rays, [1] secondary rays, [2..8] work counters (kCounterWords)
+    unsigned long long* wave_times;  // debug (rt_debug_wave_times): per wave {start, end, tile} in 100 MHz ticks
 };
 
 constexpr int kCounterWords = 16;   // u64 words behind RenderParams::counters

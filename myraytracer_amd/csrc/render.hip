@@ -148,10 +148,17 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     extern __shared__ unsigned long long lds_stack[];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    // one tile = 32x8 pixels of one selected chunk; tiles are row-major over (slot, column)
-    const int gx = (P.cam.width + 31) >> 5;
-    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
-    const int i = (tile % gx) * 32 + wave * 8 + (lane & 7);
+    const unsigned long long t_start = P.wave_times ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    // one tile = (8 x waves-per-block) x 8 pixels of one selected chunk (one 8x8 square per
+    // wave); tiles are row-major over (slot, column)
+    const int wpb = (int)(blockDim.x >> 6);
+    const int gx = (P.cam.width + 8 * wpb - 1) / (8 * wpb);
+    int b = (int)blockIdx.x;
+    const int nb = (int)gridDim.x;
+    if (P.tile_order == 1) b = nb - 1 - b;
+    else if (P.tile_order == 2 && nb % 7919 != 0) b = (int)(((long long)b * 7919) % nb);   // bijective: 7919 is prime
+    const int tile = xcd_tile(b, nb, P.xcd_remap);
+    const int i = (tile % gx) * (8 * wpb) + wave * 8 + (lane & 7);
     const int slot = tile / gx;                        // position in the selected chunk list
     const int chunk = P.chunk_first + slot * P.chunk_step;
     const int rowInChunk = lane >> 3;
@@ -216,6 +223,13 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             const unsigned packed = (unsigned)(unsigned char)cx | ((unsigned)(unsigned char)cy << 8) |
                                     ((unsigned)(unsigned char)cz << 16) | (255u << 24);
             reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
+        }
+    }
+    if (P.wave_times) {                                              // debug timeline
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            unsigned long long* w = P.wave_times + 3 * ((size_t)blockIdx.x * wpb + wave);
+            w[0] = t_start; w[1] = t_end; w[2] = (unsigned long long)tile;
         }
     }
     // ray / work counters: one atomic per wave
@@ -306,6 +320,7 @@ static int32_t fail(int32_t code, const std::string& msg) { g_err = msg; return 
         if (_e != hipSuccess) return fail(RT_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
 
+constexpr int kRenderBlock = 64;    // default threads per render block (block_threads): one wave
 constexpr int kRenderBatches = 8;   // rt_render: chunk batches per replica (progress / overlap granularity)
 
 struct DeviceReplica {
@@ -325,6 +340,7 @@ struct DeviceReplica {
     long long* jstart = nullptr;
     int64_t cap_px = 0;
     unsigned long long* counters = nullptr;   // kCounterWords x u64
+    unsigned long long* wave_times = nullptr; int64_t wave_times_cap = 0;   // rt_debug_wave_times
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;        // rt_render: D2H of finished batches
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -359,7 +375,7 @@ static void free_replica(DeviceReplica& r) {
     wave_release(r.wave);
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
-    (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart);
+    (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart); (void)hipFree(r.wave_times);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -512,7 +528,9 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.stack_depth = dev::kLds;
     {
         const char* xe = std::getenv("MYRT_XCD");                // tile-group size per XCD (device.h xcd_tile)
-        P.xcd_remap = xe ? std::atoi(xe) : 0;
+        P.xcd_remap = xe ? std::atoi(xe) : 2;                   // pairs of 8x8 tiles per XCD (measured best)
+        const char* oe = std::getenv("MYRT_ORDER");              // block->tile order (A/B)
+        P.tile_order = oe ? std::atoi(oe) : 0;
         const char* se = std::getenv("MYRT_SCALAR");            // A/B switch: MYRT_SCALAR=0
         P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
         const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0
@@ -522,6 +540,7 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
+    P.wave_times = nullptr;
     P.alights = r.alights;
     P.jitter = r.jitter;
     P.num_alights = (int32_t)S.alights.size();
@@ -541,10 +560,25 @@ static bool use_megakernel() {
     return !(e && std::strcmp(e, "wave") == 0);
 }
 
+// Threads per render block.  A block's LDS and wave slots are released only when ALL of
+// its waves finish, and wave durations vary ~4x across neighbouring 8x8 tiles: with 4-wave
+// blocks ~25% of the wave slots sat idle behind a block's slowest wave
+// (tools/probe_timeline.py).  One-wave blocks free each slot as soon as its wave ends.
+static int block_threads() {
+    const char* e = std::getenv("MYRT_BLOCK");
+    const int v = e ? std::atoi(e) : kRenderBlock;
+    return (v == 64 || v == 128 || v == 256) ? v : kRenderBlock;
+}
+static dim3 render_grid(const RenderParams& P, int threads) {
+    const int px = 8 * (threads / 64);                   // pixels per block along a row
+    return dim3((unsigned)(((P.cam.width + px - 1) / px) * P.num_chunks), 1, 1);
+}
+
 static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count) {
-    dim3 grid((unsigned)(((P.cam.width + 31) / 32) * P.num_chunks), 1, 1);
-    dim3 block(256, 1, 1);
-    const size_t lds = (size_t)dev::kLds * 256 * sizeof(unsigned long long);
+    const int bt = block_threads();
+    dim3 grid = render_grid(P, bt);
+    dim3 block((unsigned)bt, 1, 1);
+    const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long);
     if (P.num_alights > 0) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
         if (px > r.cap_px) {
@@ -558,7 +592,7 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
         P.events = r.events;
         P.jstart = r.jstart;
         hipLaunchKernelGGL(dev::k_events, grid, block, lds, stream, P);
-        hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), block, 0, stream, P);
+        hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), dim3(256, 1, 1), 0, stream, P);
     }
     if (count) hipLaunchKernelGGL((dev::render_full<true>), grid, block, lds, stream, P);
     else hipLaunchKernelGGL((dev::render_full<false>), grid, block, lds, stream, P);
@@ -579,9 +613,10 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
                                                          : "wavefront launch failed");
         return RT_OK;
     }
-    dim3 grid((unsigned)(((P.cam.width + 31) / 32) * P.num_chunks), 1, 1);
-    dim3 block(256, 1, 1);
-    const size_t lds = (size_t)dev::kLds * 256 * sizeof(int2);
+    const int bt = block_threads();
+    dim3 grid = render_grid(P, bt);
+    dim3 block((unsigned)bt, 1, 1);
+    const size_t lds = (size_t)dev::kLds * bt * sizeof(int2);
     const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
     // the unified walk needs an identity scene; reference-order counting uses the general walk
     const char* ue = std::getenv("MYRT_UNIFIED");
@@ -1137,6 +1172,34 @@ int32_t rt_debug_occluded_rays(rt_scene* s, int32_t slot, int32_t n, const doubl
 }
 
 // ---- debug: canonical BVH hashes (tests compare them with the oracle's)
+int32_t rt_debug_wave_times(rt_scene* s, int32_t slot, int32_t cam, int32_t first, int32_t step, double* d_out_rgb,
+                            uint64_t* out, int64_t max_waves, int64_t* n_waves) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+    if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
+    int32_t rc = check_renderable(s->host, cam);
+    if (rc != RT_OK) return rc;
+    std::lock_guard<std::mutex> lock(s->mu);
+    DeviceReplica& r = s->devs[slot];
+    HIP_TRY(hipSetDevice(r.device));
+    RenderParams P = make_params(s, r, cam, first, step, d_out_rgb, nullptr);
+    const int bt = block_threads();
+    const int64_t waves = (int64_t)render_grid(P, bt).x * (bt / 64);
+    if (waves > r.wave_times_cap) {
+        (void)hipFree(r.wave_times); r.wave_times = nullptr; r.wave_times_cap = 0;
+        HIP_TRY(hipMalloc((void**)&r.wave_times, (size_t)waves * 3 * sizeof(unsigned long long)));
+        r.wave_times_cap = waves;
+    }
+    HIP_TRY(hipMemsetAsync(r.wave_times, 0, (size_t)waves * 3 * sizeof(unsigned long long), r.stream));
+    P.wave_times = r.wave_times;
+    HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
+    if ((rc = launch(s, r, P, r.stream, false)) != RT_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    const int64_t n = std::min<int64_t>(waves, max_waves);
+    if (out && n > 0) HIP_TRY(hipMemcpy(out, r.wave_times, (size_t)n * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (n_waves) *n_waves = waves;
+    return RT_OK;
+}
+
 uint64_t rt_debug_bvh_hash(const rt_scene* s, int32_t instance) {
     if (!s) return 0;
     if (instance < 0) return s->host.tlas_hash;

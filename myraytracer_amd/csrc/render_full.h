@@ -285,9 +285,10 @@ __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, lo
 
 __device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int& j, int& slot, int& row) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int gx = (P.cam.width + 31) >> 5;
+    const int wpb = (int)(blockDim.x >> 6);
+    const int gx = (P.cam.width + 8 * wpb - 1) / (8 * wpb);
     const int tile = (int)blockIdx.x;
-    i = (tile % gx) * 32 + wave * 8 + (lane & 7);
+    i = (tile % gx) * (8 * wpb) + wave * 8 + (lane & 7);
     slot = tile / gx;
     const int chunk = P.chunk_first + slot * P.chunk_step;
     row = lane >> 3;

@@ -1,0 +1,43 @@
+"""Kernel time of the C3 (or C5) frame under runtime switch combinations (A/B in one process).
+usage: probe_env.py c3 "MYRT_BLOCK=64 MYRT_XCD=4" "MYRT_BLOCK=64 MYRT_ORDER=1" ..."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+import myraytracer_amd as M
+from myraytracer_amd import scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+cfg = sys.argv[1]
+sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache")) if cfg == "c3" else \
+    scenes.scene_c5(path_dir=os.path.join(ROOT, "scenes_cache"))
+eng = M.RayTracerEngine(sc)
+W, H = sc.cameras[0].image_resolution
+stream = torch.cuda.current_stream()
+out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ORDER", "MYRT_SCALAR", "MYRT_COMPACT", "MYRT_CTRI")
+
+
+def t_frame(k=20):
+    for _ in range(3):
+        eng.render_device(out.data_ptr(), 0, 0, 1, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(k):
+        eng.render_device(out.data_ptr(), 0, 0, 1, stream=stream.cuda_stream)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / k
+
+
+for rep in range(2):
+    for combo in sys.argv[2:]:
+        for key in KEYS:
+            os.environ.pop(key, None)
+        for kv in combo.split():
+            k, v = kv.split("=")
+            os.environ[k] = v
+        print(f"{cfg} [{combo}] {t_frame():.4f} ms", flush=True)
