@@ -129,6 +129,9 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 
 
 // One block = 256 lanes = 4 waves; each wave renders an 8x8 tile of one 8-row chunk.
+#ifndef MYRT_WAVE_TIMES
+#define MYRT_WAVE_TIMES 0    // per-wave timeline for rt_debug_wave_times (debug builds only: costs SGPRs)
+#endif
 #ifndef MYRT_MEGA_WPE
 #define MYRT_MEGA_WPE 4      // amdgpu_waves_per_eu for the megakernel (0 = compiler default = 2 waves at ~200 VGPRs)
 #endif
@@ -148,16 +151,14 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     extern __shared__ unsigned long long lds_stack[];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const unsigned long long t_start = P.wave_times ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#if MYRT_WAVE_TIMES
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     // one tile = (8 x waves-per-block) x 8 pixels of one selected chunk (one 8x8 square per
     // wave); tiles are row-major over (slot, column)
     const int wpb = (int)(blockDim.x >> 6);
     const int gx = (P.cam.width + 8 * wpb - 1) / (8 * wpb);
-    int b = (int)blockIdx.x;
-    const int nb = (int)gridDim.x;
-    if (P.tile_order == 1) b = nb - 1 - b;
-    else if (P.tile_order == 2 && nb % 7919 != 0) b = (int)(((long long)b * 7919) % nb);   // bijective: 7919 is prime
-    const int tile = xcd_tile(b, nb, P.xcd_remap);
+    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
     const int i = (tile % gx) * (8 * wpb) + wave * 8 + (lane & 7);
     const int slot = tile / gx;                        // position in the selected chunk list
     const int chunk = P.chunk_first + slot * P.chunk_step;
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
         }
     }
+#if MYRT_WAVE_TIMES
     if (P.wave_times) {                                              // debug timeline
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
@@ -232,6 +234,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             w[0] = t_start; w[1] = t_end; w[2] = (unsigned long long)tile;
         }
     }
+#endif
     // ray / work counters: one atomic per wave
     const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary);
     if (lane == 0) {
@@ -529,8 +532,6 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     {
         const char* xe = std::getenv("MYRT_XCD");                // tile-group size per XCD (device.h xcd_tile)
         P.xcd_remap = xe ? std::atoi(xe) : 2;                   // pairs of 8x8 tiles per XCD (measured best)
-        const char* oe = std::getenv("MYRT_ORDER");              // block->tile order (A/B)
-        P.tile_order = oe ? std::atoi(oe) : 0;
         const char* se = std::getenv("MYRT_SCALAR");            // A/B switch: MYRT_SCALAR=0
         P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
         const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0
@@ -1174,6 +1175,9 @@ int32_t rt_debug_occluded_rays(rt_scene* s, int32_t slot, int32_t n, const doubl
 // ---- debug: canonical BVH hashes (tests compare them with the oracle's)
 int32_t rt_debug_wave_times(rt_scene* s, int32_t slot, int32_t cam, int32_t first, int32_t step, double* d_out_rgb,
                             uint64_t* out, int64_t max_waves, int64_t* n_waves) {
+    if (!MYRT_WAVE_TIMES)
+        return fail(RT_ERR_UNSUPPORTED, "wave timeline not compiled in (build with -DMYRT_WAVE_TIMES=1, "
+                                        "tools/build_variants.sh)");
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
     if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
     int32_t rc = check_renderable(s->host, cam);
