@@ -13,6 +13,7 @@ from myraytracer_amd import scenes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+TAG = os.environ.get("MYRT_ORDER", "0")
 sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache")) if cfg == "c3" else \
     scenes.scene_c5(path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
@@ -46,13 +47,17 @@ print("resident waves every 5% of the span:", " ".join(str(int(a)) for a in act[
 # waves that start in the last 25% of the span and their durations
 late = st > 0.75 * span
 print(f"waves starting in the last 25%: {late.sum()}, mean duration {dur[late].mean() if late.any() else 0:.4f} ms", flush=True)
-gx = (W + 31) // 32
+wpb = int(os.environ.get("MYRT_BLOCK", "64")) // 64
+gx = (W + 8 * wpb - 1) // (8 * wpb)
 top = np.argsort(-dur)[:10]
 for k in top:
-    blk = int(tile[k]); wv = int(k % 4)
-    print(f"  slow wave: tile {blk} (px x {(blk % gx) * 32 + wv * 8}, chunk {blk // gx}) start {st[k]:.4f} dur {dur[k]:.4f} ms")
+    blk = int(tile[k]); wv = int(k % wpb)
+    print(f"  slow wave: tile {blk} (px x {(blk % gx) * 8 * wpb + wv * 8}, chunk {blk // gx}) start {st[k]:.4f} dur {dur[k]:.4f} ms")
 # per-chunk mean duration (image rows)
 ch = tile // gx
 cm = np.bincount(ch, weights=dur) / np.maximum(np.bincount(ch), 1)
-print("mean wave duration per 8-row chunk (every 8th):", " ".join(f"{x:.3f}" for x in cm[::8]), flush=True)
-np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{cfg}.npy"), t)
+print("mean wave duration per 8-row chunk (every 4th):", " ".join(f"{x:.3f}" for x in cm[::4]), flush=True)
+# start time of each chunk's first wave (dispatch progress)
+cs = np.array([st[ch == c].min() if (ch == c).any() else 0 for c in range(ch.max() + 1)])
+print("first start per chunk (every 8th, ms):", " ".join(f"{x:.3f}" for x in cs[::8]), flush=True)
+np.save(os.path.join(ROOT, "gpurun_out", f"timeline_{cfg}_o{TAG}.npy"), t)
