@@ -129,9 +129,11 @@ struct Stack {
     priv_u64* spill;     // kSpill private entries
     int stride;
     int sp;
+    __device__ __forceinline__ static unsigned long long pack(int ref, double t) {
+        return (unsigned long long)(unsigned)ref | ((unsigned long long)(unsigned)__double2hiint(t) << 32);
+    }
     __device__ __forceinline__ void push(int ref, double t) {
-        const unsigned long long e = (unsigned long long)(unsigned)ref |
-                                     ((unsigned long long)(unsigned)__double2hiint(t) << 32);
+        const unsigned long long e = pack(ref, t);
         if (sp < kLds) {
             lds[sp * stride] = e;
         } else {
@@ -143,8 +145,7 @@ struct Stack {
     // push when `keep`; the LDS store is issued regardless (slot sp is free), only the
     // rare spill store is conditional
     __device__ __forceinline__ void push_if(bool keep, int ref, double t) {
-        const unsigned long long e = (unsigned long long)(unsigned)ref |
-                                     ((unsigned long long)(unsigned)__double2hiint(t) << 32);
+        const unsigned long long e = pack(ref, t);
         if (sp < kLds) {
             lds[sp * stride] = e;
         } else if (keep) {
@@ -164,6 +165,8 @@ struct Stack {
         tlo = __hiloint2double((int)(unsigned)(e >> 32), 0);
         return (int)(unsigned)(e & 0xffffffffull);
     }
+    // drop every entry above `base`
+    __device__ __forceinline__ void reset(int base) { sp = base; }
 };
 #define MYRT_STACK(name, lds_base)                                   \
     unsigned long long name##_spill_mem[kSpill];                     \
@@ -553,7 +556,7 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
                 auto blas_leaf = [&](int r) -> bool {
                     auto run = [&](const auto* tris) {
                         for (int t = ~r;; ++t) {
-                            const auto& T = tris[t];
+                            const auto T = tris[t];          // by value: `last` arrives with the vertices
                             if (COUNT) c.tris++;
                             const bool closer = tri_closest(T, omb, dl, tlo, eps, h, t, inst);
                             if (MYRT_REF(P) && closer && I.smooth) c.smooth++;
@@ -611,7 +614,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
                 auto blas_leaf = [&](int r) -> bool {
                     auto run = [&](const auto* tris) -> bool {
                         for (int t = ~r;; ++t) {
-                            const auto& T = tris[t];
+                            const auto T = tris[t];          // by value: `last` arrives with the vertices
                             if (COUNT) c.tris++;
                             if (tri_shadow(T, omb, dl, 0.0, tmax, eps)) return true;
                             if (T.last) break;
@@ -625,7 +628,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
                 if (I.kind != kPrimTriangles) hit = prim_shadow(I.kind, P.tris[~I.root_ref], ol, dl, tmax, eps);
                 else if (I.root_ref < 0) hit = blas_leaf(I.root_ref);
                 else hit = walk_any<COUNT, true>(P, I.root_ref, ol, il, st, sbase, c, blas_leaf, limit);
-                if (hit) { st.sp = sbase; return true; }
+                if (hit) { st.reset(sbase); return true; }
             }
             if (le.last) break;
         }
@@ -635,7 +638,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
     bool hit;
     if (P.tlas_root_ref < 0) hit = tlas_leaf(P.tlas_root_ref);
     else hit = walk_any<COUNT, true>(P, P.tlas_root_ref, o, inv, st, base, c, tlas_leaf, limit);
-    st.sp = base;
+    st.reset(base);
     return hit;
 }
 
@@ -655,15 +658,16 @@ __device__ __forceinline__ bool unified_leaf(const RenderParams& P, int ref, Sta
     const double eps = P.eps;
     const int e = ~ref;
     if (e < P.tlas_leaf_base) {                                  // BLAS leaf run
+        auto test = [&](const auto& T, int t) -> bool {
+            if (COUNT) c.tris++;
+            if (SHADOW) return tri_shadow(T, o, d, 0.0, tmax, eps);
+            tri_closest(T, o, d, tlo, eps, h, t, T.prim);            // prim = owning instance
+            return false;
+        };
         auto run = [&](const auto* tris) -> bool {
             for (int t = e;; ++t) {
-                const auto& T = tris[t];
-                if (COUNT) c.tris++;
-                if (SHADOW) {
-                    if (tri_shadow(T, o, d, 0.0, tmax, eps)) return true;
-                } else {
-                    tri_closest(T, o, d, tlo, eps, h, t, T.prim); // prim = owning instance
-                }
+                const auto T = tris[t];          // by value: `last` arrives with the vertices
+                if (test(T, t)) return true;
                 if (T.last) break;
             }
             return false;
@@ -701,7 +705,7 @@ __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Sta
         // pays for at most one record and one triangle
         const int t = ~ref;
         auto one = [&](const auto* tris) -> int {
-            const auto& T = tris[t];
+            const auto T = tris[t];          // by value: `last` arrives with the vertices
             if (COUNT) c.tris++;
             if (SHADOW) {
                 if (tri_shadow(T, o, d, 0.0, tmax, P.eps)) return 2;
@@ -791,7 +795,7 @@ __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V
     } else {
         do { if (COUNT) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0);
     }
-    st.sp = base;
+    st.reset(base);
     return r == 2;
 }
 template <bool COUNT>

@@ -130,7 +130,7 @@ struct RenderParams {
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
     int32_t scalar_nodes;            // wave-uniform records via scalar loads (device.h inner_step)
     int32_t compact_limit;           // records below this index are read from crecs
-    int32_t pad2;
+    int32_t rot_slots;               // megakernel dispatch order: selected chunk rows rotated by this many
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)

@@ -158,13 +158,12 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     // wave); tiles are row-major over (slot, column)
     const int wpb = (int)(blockDim.x >> 6);
     const int gx = (P.cam.width + 8 * wpb - 1) / (8 * wpb);
-#if MYRT_WAVE_TIMES
-    // debug builds only: block->tile order experiments (P.pad2: 1 = reversed)
-    const int tile = xcd_tile(P.pad2 == 1 ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x, (int)gridDim.x,
-                              P.xcd_remap);
-#else
-    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
-#endif
+    int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
+    // rotated dispatch order: the first rot_slots chunk rows go last (host: MYRT_ROTATE)
+    if (P.rot_slots > 0) {
+        tile += P.rot_slots * gx;
+        if (tile >= (int)gridDim.x) tile -= (int)gridDim.x;
+    }
     const int i = (tile % gx) * (8 * wpb) + wave * 8 + (lane & 7);
     const int slot = tile / gx;                        // position in the selected chunk list
     const int chunk = P.chunk_first + slot * P.chunk_step;
@@ -540,8 +539,8 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         // runs of G neighbouring 8x8 tiles per XCD; measured best: G = 2 at 1920 px (C3),
         // G = 4 at 3840 px (C5), i.e. about one run per 960 px of image width
         P.xcd_remap = xe ? std::atoi(xe) : std::max(2, P.cam.width / 960);
-        const char* oe = std::getenv("MYRT_ORDER");              // debug builds: tile order (P.pad2)
-        P.pad2 = (MYRT_WAVE_TIMES && oe) ? std::atoi(oe) : 0;
+        const char* oe = std::getenv("MYRT_ROTATE");             // dispatch order: chunk rows rotated
+        P.rot_slots = oe ? std::max(0, std::min(std::atoi(oe), nsel - 1)) : 0;
         const char* se = std::getenv("MYRT_SCALAR");            // A/B switch: MYRT_SCALAR=0
         P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
         const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0

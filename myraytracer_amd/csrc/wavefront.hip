@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void k_persist(WaveParams W, int64_t N, unsign
                     rays++;
                     inv = rcp(d);
                     h.t = DINF; h.u = 0; h.v = 0; h.tri = -1; h.inst = -1;
-                    st.sp = 0;
+                    st.reset(0);
                     live = unified_begin(P, o, inv, SHADOW ? tmax * P.prune_rel + P.prune_abs : DINF, ref);
                     if (!live) {                                   // missed the whole scene
                         if (SHADOW) W.occluded[slot] = 0;

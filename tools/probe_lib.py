@@ -1,0 +1,44 @@
+"""Kernel time of the C3 (or C5) frame for several builds of libmyrt.so (A/B on one box).
+usage: probe_lib.py c3 myraytracer_amd/libmyrt.so build_variants/libmyrt_X.so ...
+Each library runs in its own subprocess (a process binds one libmyrt)."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) > 2 and sys.argv[2] == "--child":
+    sys.path.insert(0, ROOT)
+    import torch
+    import myraytracer_amd as M
+    from myraytracer_amd import scenes
+    cfg = sys.argv[1]
+    sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache")) if cfg == "c3" else \
+        scenes.scene_c5(path_dir=os.path.join(ROOT, "scenes_cache"))
+    eng = M.RayTracerEngine(sc)
+    W, H = sc.cameras[0].image_resolution
+    out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    res = []
+    for rep in range(3):
+        for _ in range(3):
+            eng.render_device(out.data_ptr(), 0, 0, 1, stream=s)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            eng.render_device(out.data_ptr(), 0, 0, 1, stream=s)
+        e1.record()
+        torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) / 20)
+    import hashlib
+    h = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
+    print(f"{cfg} {os.path.basename(os.environ['MYRT_LIB'])}: " + " ".join(f"{x:.4f}" for x in res)
+          + f" ms  (min {min(res):.4f})  frame sha1 {h}", flush=True)
+    sys.exit(0)
+cfg = sys.argv[1]
+for rnd in range(2):
+    for lib in sys.argv[2:]:
+        env = dict(os.environ, MYRT_LIB=os.path.abspath(lib))
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), cfg, "--child"], env=env)
+        if r.returncode != 0:
+            sys.exit(r.returncode)
