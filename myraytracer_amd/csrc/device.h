@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "layout.h"
+#include "slab32.h"
 
 namespace myrt {
 namespace dev {
@@ -800,12 +801,165 @@ __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3
     }
     do { if (COUNT) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0);
 }
+// ------------------------------------------------------------ FP32-enclosed walks (MYRT_F32)
+// The reference's slab test is FP64 (hitAABB, RTContext.swift:557-565).  A wave64 FP32 op
+// issues in 2 cycles on gfx950 and an FP64 op in 4, and the FP64 test of a compact record
+// also needs 12 v_cvt_f64_f32.  For rays with no zero direction component these walks test
+// compact records in FP32 with a bound that encloses the FP64 values (slab32.h) and take a
+// decision in FP32 only when the enclosure makes it certain:
+//   * an uncertain hit/miss is recomputed in FP64 for that child, so every visited node is
+//     one the reference visits (pruning aside);
+//   * an uncertain near/far order is taken from the FP32 values and remembered: the order
+//     only decides which of two EQUAL-t triangle hits wins (H2; pruning never removes the
+//     closest hit's node), so a ray that took an uncertain order AND met an equal-t
+//     candidate is walked again in the exact FP64 order;
+//   * any-hit walks are unordered (MYRT_SHADOW_ORDER) and need only hit/miss.
+// Measured slower (C3 0.92 vs 0.79 ms/frame, C5 4.16 vs 3.45; not yet profiled, the extra
+// enclosure state per lane is the suspect), so they are compiled out by default: build with
+// -DMYRT_F32=1 to include them; RenderParams::use_f32 = 0 (host: MYRT_F32=0) then selects FP64.
+#ifndef MYRT_F32
+#define MYRT_F32 0
+#endif
+template <bool SHADOW, class Rec>
+__device__ __forceinline__ bool inner_step_f32(const RenderParams& P, const Rec& R, int& ref, const V3& o,
+                                               const V3& d, const f32slab::RayF& F, float lim_up, Stack& st,
+                                               bool& amb) {
+    float m0, lo0, hi0, m1, lo1, hi1;
+    int c0 = f32slab::test(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], F, P.eps_up32,
+                           P.eps_dn32, m0, lo0, hi0);
+    int c1 = f32slab::test(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], F, P.eps_up32,
+                           P.eps_dn32, m1, lo1, hi1);
+    if (c0 < 0 || c1 < 0) {                 // rare: the reference's FP64 test for that child
+        const V3 inv = rcp(d);
+        double t;
+        if (c0 < 0) {
+            c0 = slab_hit<true>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
+                                P.eps, t) ? 1 : 0;
+            f32slab::enclose(t, m0, lo0, hi0);
+        }
+        if (c1 < 0) {
+            c1 = slab_hit<true>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
+                                P.eps, t) ? 1 : 0;
+            f32slab::enclose(t, m1, lo1, hi1);
+        }
+    }
+    const bool h0 = c0 > 0 && !(lo0 > lim_up);     // lo <= FP64 tmin: prunes only what FP64 would
+    const bool h1 = c1 > 0 && !(lo1 > lim_up);
+    const int a = R.ref[0], b = R.ref[1];
+    const bool both = h0 && h1;
+    bool sw = false;
+    if (!SHADOW) {
+        const bool yes = lo0 > hi1, no = hi0 <= lo1;  // certainly t0 > t1 / certainly not
+        sw = yes || (!no && m0 > m1);
+        amb = amb || (both && !yes && !no);
+    }
+    st.push_if(both, sw ? a : b, (double)(sw ? lo0 : lo1));
+    ref = both ? (sw ? b : a) : (h0 ? a : b);
+    return h0 || h1;
+}
+template <bool SHADOW>
+__device__ __forceinline__ bool inner_step_f32_any(const RenderParams& P, int& ref, const V3& o, const V3& d,
+                                                   const f32slab::RayF& F, float lim_up, Stack& st, bool& amb) {
+    const int r0 = __builtin_amdgcn_readfirstlane(ref);
+    if (P.scalar_nodes && __all(ref == r0))
+        return inner_step_f32<SHADOW>(P, load_crec_scalar(P.crecs + r0), ref, o, d, F, lim_up, st, amb);
+    return inner_step_f32<SHADOW>(P, P.crecs[ref], ref, o, d, F, lim_up, st, amb);
+}
+// tri_closest that also reports an equal-t candidate
+template <class Tri>
+__device__ __forceinline__ void tri_closest_tie(const Tri& T, const V3& o_mb, const V3& d, double tlo, double eps,
+                                                Hit& h, int triIdx, int instIdx, bool& tie) {
+    V3 v0, e1, e2;
+    tri_geom(T, v0, e1, e2);
+    const V3 pvec = cross(d, e2);
+    const double det = dot(e1, pvec);
+    if (fabs(det) < eps) return;
+    const double invDet = 1.0 / det;
+    const V3 tvec = o_mb - v0;
+    const double u = dot(tvec, pvec) * invDet;
+    if (u < 0.0 || u > 1.0) return;
+    const V3 q = cross(tvec, e1);
+    const double v = dot(d, q) * invDet;
+    if (v < 0.0 || u + v > 1.0) return;
+    const double t = dot(e2, q) * invDet;
+    if (t <= smax(eps, tlo)) return;
+    if (t >= h.t) { tie = tie || (t == h.t); return; }
+    h.t = t; h.u = u; h.v = v; h.tri = triIdx; h.inst = instIdx;
+}
+template <bool SHADOW>
+__device__ __forceinline__ int unified_step_f32(const RenderParams& P, int& ref, Stack& st, const V3& o, const V3& d,
+                                                const f32slab::RayF& F, double tlo, double tmax, Hit& h, bool& amb,
+                                                bool& tie, float& lim32, Counts& c) {
+    if (ref >= 0) {
+        if (ref < P.compact_limit) {
+            if (inner_step_f32_any<SHADOW>(P, ref, o, d, F, lim32, st, amb)) return 0;
+        } else if (inner_step<false, true, SHADOW>(P, ref, o, rcp(d),
+                                                   (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c)) {
+            return 0;                                 // full FP64 records (TLAS): the exact step
+        }
+    } else {
+        const int e = ~ref;
+        if (e < P.tlas_leaf_base) {                   // BLAS leaf run
+            auto run = [&](const auto* tris) -> bool {
+                for (int t = e;; ++t) {
+                    const auto T = tris[t];
+                    if (SHADOW) {
+                        if (tri_shadow(T, o, d, 0.0, tmax, P.eps)) return true;
+                    } else {
+                        tri_closest_tie(T, o, d, tlo, P.eps, h, t, T.prim, tie);
+                    }
+                    if (T.last) break;
+                }
+                return false;
+            };
+            if (P.ctris ? run(P.ctris) : run(P.tris)) return 2;
+            if (!SHADOW) lim32 = f32slab::up(h.t * P.prune_rel + P.prune_abs);
+        } else if (unified_leaf<false, SHADOW, true>(P, ref, st, o, d, rcp(d), tlo, tmax, h, c)) {
+            return 2;                                 // TLAS leaf: instance roots in FP64
+        }
+    }
+    return pop_next<false, SHADOW>(P, st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref, c) ? 0 : 1;
+}
+__device__ __forceinline__ void uni_closest_f32(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
+                                                double tlo, Hit& h, Stack& st, Counts& c) {
+    int ref;
+    if (!unified_begin(P, o, inv, DINF, ref)) return;
+    const f32slab::RayF F = f32slab::make(o.x, o.y, o.z, inv.x, inv.y, inv.z, P.bmax32);
+    bool amb = false, tie = false;
+    float lim32 = __builtin_inff();
+    while (unified_step_f32<false>(P, ref, st, o, d, F, tlo, DINF, h, amb, tie, lim32, c) == 0) {}
+    if (amb && tie) {                               // equal-t hits after an uncertain order
+        h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+        st.reset(0);
+        uni_closest_walk<false, true>(P, o, d, rcp(d), tlo, h, st, c);
+    }
+}
+__device__ __forceinline__ bool uni_occluded_f32(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
+                                                 double tmax, Stack& st, Counts& c) {
+    int ref;
+    if (!unified_begin(P, o, inv, tmax * P.prune_rel + P.prune_abs, ref)) return false;
+    const f32slab::RayF F = f32slab::make(o.x, o.y, o.z, inv.x, inv.y, inv.z, P.bmax32);
+    Hit h;                                           // unused by any-hit steps
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    bool amb = false, tie = false;
+    float lim32 = f32slab::up(tmax * P.prune_rel + P.prune_abs);
+    const int base = st.sp;
+    int r;
+    while ((r = unified_step_f32<true>(P, ref, st, o, d, F, 0.0, tmax, h, amb, tie, lim32, c)) == 0) {}
+    st.reset(base);
+    return r == 2;
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
                                             double tlo, Hit& h, Stack& st, Counts& c) {
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-    if (__all(finite3(inv))) uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
-    else uni_closest_walk<COUNT, false>(P, o, d, inv, tlo, h, st, c);
+    if (__all(finite3(inv))) {
+        if (MYRT_F32 && !COUNT && P.use_f32) uni_closest_f32(P, o, d, inv, tlo, h, st, c);
+        else uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
+    } else {
+        uni_closest_walk<COUNT, false>(P, o, d, inv, tlo, h, st, c);
+    }
 }
 template <bool COUNT, bool FAST>
 __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
@@ -829,7 +983,10 @@ __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o,
                                              Stack& st, Counts& c) {
     if (!P.has_tlas) return false;
     const V3 inv = rcp(d);
-    if (__all(finite3(inv))) return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
+    if (__all(finite3(inv))) {
+        if (MYRT_F32 && !COUNT && P.use_f32) return uni_occluded_f32(P, o, d, inv, tmax, st, c);
+        return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
+    }
     return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);
 }
 

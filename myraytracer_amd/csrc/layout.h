@@ -122,6 +122,9 @@ struct RenderParams {
     DCamera cam;
     double eps, shadow_eps;
     double prune_rel, prune_abs;     // conservative t-pruning margins (DESIGN.md "H3")
+    float eps_up32, eps_dn32;        // eps rounded out to floats (slab32.h)
+    float bmax32;                    // >= every |coordinate| of the scene (slab32.h overflow guard)
+    int32_t use_f32;                 // FP32-enclosed slab walks (device.h MYRT_F32; host MYRT_F32=0 disables)
     double background[3], ambient[3];
     int32_t max_depth;
     int32_t chunk_first, chunk_step, num_chunks;   // selected 8-row chunks

@@ -527,6 +527,17 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.eps = S.eps; P.shadow_eps = S.shadow_eps;
     P.prune_rel = 1.0 + 1e-7;
     P.prune_abs = 1e-9 * S.scene_extent;
+    {   // FP32-enclosed slabs (slab32.h): eps rounded out, and a bound on every coordinate of an
+        // identity scene (every box of the unified walk lies inside the TLAS root box)
+        P.eps_up32 = f32slab::up(P.eps);
+        P.eps_dn32 = f32slab::dn(P.eps);
+        double bm = 0.0;
+        for (int k = 0; k < 3; ++k)
+            bm = std::max(bm, std::max(std::fabs(S.tlas_root_lo[k]), std::fabs(S.tlas_root_hi[k])));
+        P.bmax32 = f32slab::up(bm);
+        const char* fe = std::getenv("MYRT_F32");
+        P.use_f32 = (fe && fe[0] == '0') ? 0 : 1;
+    }
     for (int k = 0; k < 3; ++k) { P.background[k] = S.background[k]; P.ambient[k] = S.ambient[k]; }
     P.max_depth = S.max_depth;
     P.chunk_first = first; P.chunk_step = step;
