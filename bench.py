@@ -3,30 +3,49 @@
 
 Workload (BASELINE.json configs[2], "C3"): a ~1.02M-triangle single-mesh PLY scene
 (512^2 heightfield + 24 icospheres, seeded; no Stanford bunny exists offline),
-1920x1080, 1 spp, 1 point light, shadow rays on.  One "step" = one full frame of the
-hot path (primary ray generation, TLAS/BLAS traversal, Moeller-Trumbore, Whitted
-shading with shadow rays), FP64, scene and output resident in HBM.
+1920x1080, 1 spp, 1 point light, shadow rays on, FP64 throughout.
 
-N GPUs (torchrun, one process per GPU): pixels are independent (each seeds its own
-PCG32), so the path shards with no collective on the data path.  Default
-`--scaling weak` (the contract for a partitioned path): every rank renders one full C3
-frame per step from its own scene replica - per-GPU work is fixed as N grows.
-`--scaling strong` is configs[3] "C4": ONE frame, 8-row chunk c on rank c mod N.
+One "step" = one frame through the public render path, timed as SURVEY.md §8(d) defines
+it: `rt_render` wall time with the scene resident in HBM, INCLUDING the device->host
+delivery of the image and the host gather.  The image is what the reference's public
+`RayTracerEngine.render` returns - RGBA8 (RayTracer.swift:115-131, 166-203: its render
+time spans Renderer.render + the RGBA8 conversion).  The kernels store the RGBA8 rows
+straight into a page-locked host framebuffer (host-mapped, over PCIe).  Side fields time
+the FP64 [Vec3] framebuffer delivered the same way (`fp64_path`) and the device-only
+launch (`device_only`).
 
-Timed region: K frames bracketed by barrier + device sync; value = (primary + shadow
-rays of all ranks) / max-over-ranks wall time.  Roofline: algorithmic
-bytes B = 56 N_nodeFetch + 72 N_triTest + 72 N_smoothHit + 24 N_pixel counted in the
-reference's traversal order by a counting launch (equal to the oracle's tally), divided
-by the average frame time from HIP events on the launch stream; `traffic` = PMC HBM
-bytes per launch from profiles/traffic_<config>.json (tools/pmc_traffic.py).
+N GPUs: one process per GPU (torchrun; `python bench.py --gpus N` starts torchrun itself
+before anything touches a GPU).  Default for N>1 is configs[3] "C4", STRONG scaling: ONE
+C3 frame per step, 8-row chunk c rendered by rank c mod N (Object+Extension.swift:75-82),
+every rank storing its rows into one shared page-locked framebuffer (POSIX shared memory
+registered with rt_host_register) - the host-side gather, with no collective on the data
+path.  `--scaling weak` (opt-in) gives every rank a full frame of its own.
+
+value = (primary rays + shadow rays actually traversed, all ranks) / max-over-ranks wall
+time of K steps bracketed by barrier + device sync.  Shadow rays whose walk is skipped
+(N.L <= 0: the reference discards their result, Object+Extension.swift:123-141) are
+reported apart (`rays.shadow_cast`), never in `value`.
+
+roofline (dominant kernel = the render megakernel, average duration from HIP events on
+its stream, taken inside rt_render): `achieved` = measured HBM bytes per launch (PMC
+FETCH_SIZE x2 + WRITE_SIZE, profiles/roofline_<config>.json, same build) / kernel time,
+against the 8 TB/s HBM peak.  The kernel is not HBM-bound (its working set sits in L2 and
+the 256 MB Infinity Cache): `roofline.binding` names the resource that binds it (the
+vector-memory data path, TD busy from the same profile) and `roofline.reference_work` the
+SURVEY §8(d) algorithmic bytes of the reference's unpruned walk, counted on the GPU.
 cpu_baseline: the C++ restatement of the reference CPU renderer (oracle/, test
-infrastructure) on a bounded sample of the same frame, rank 0, N = 1.
+infrastructure), rank 0, N = 1: median over whole frames at the box's CPU share, plus the
+1-thread rate on a sampled subset of chunks.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import mmap
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -39,18 +58,19 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip ta
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
-    p.add_argument("--scaling", default="weak", choices=["strong", "weak"],
-                   help="strong: one frame tile-partitioned over ranks (C4); weak: every rank renders a full frame")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                   help="strong (default): one frame per step split over the ranks (C4); "
+                        "weak: every rank renders a full frame per step")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-host-path", action="store_true", help="skip the rt_render (host buffer) measurement")
-    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
+    p.add_argument("--no-side-paths", action="store_true", help="skip the fp64 / device-only side measurements")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share (OMP_NUM_THREADS / affinity)")
+    p.add_argument("--cpu-frames", type=int, default=3)
     p.add_argument("--cache", default=os.path.join(ROOT, "scenes_cache"))
-    p.add_argument("--traffic-json", default="auto",
-                   help="PMC traffic summary (tools/pmc_traffic.py output); auto = profiles/traffic_<config>.json")
+    p.add_argument("--profile-json", default="auto",
+                   help="PMC summary (tools/pmc_roofline.py); auto = profiles/roofline_<config>.json")
     return p.parse_args()
 
 
@@ -58,16 +78,62 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def relaunch_under_torchrun(args) -> int:
+    """`bench.py --gpus N` outside torchrun: start one process per GPU as a child (before any
+    GPU call in this process) and return its exit code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("[bench] starting", " ".join(cmd))
+    return subprocess.call(cmd)
+
+
+class SharedFrame:
+    """One host framebuffer shared by every rank (POSIX shared memory), page-locked in each
+    process with rt_host_register so the kernels of every GPU store their rows into it."""
+
+    def __init__(self, nbytes, rank, world, dist, tag):
+        import numpy as np
+        run = os.environ.get("TORCHELASTIC_RUN_ID", "") + os.environ.get("MASTER_PORT", "")
+        self.path = f"/dev/shm/myrt_bench_{tag}_{hashlib.sha256(run.encode()).hexdigest()[:12]}"
+        self.rank, self.world = rank, world
+        if rank == 0:
+            with open(self.path, "wb") as fh:
+                fh.truncate(nbytes)
+        if world > 1:
+            dist.barrier()
+        self._fh = open(self.path, "r+b")
+        self._mm = mmap.mmap(self._fh.fileno(), nbytes)
+        self.array = np.frombuffer(self._mm, dtype=np.uint8)   # zero-filled by the truncate
+
+    def close(self, dist):
+        import myraytracer_amd as M
+        M.unregister_host(self.array)      # the mapping itself goes with the process
+        if self.world > 1:
+            dist.barrier()
+        if self.rank == 0:
+            os.unlink(self.path)
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_under_torchrun(args))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
+        dist.init_process_group("gloo", init_method="env://")   # barriers + scalar reductions only
     # MYRT_BENCH_DEVICE pins every rank to one device: rehearsing N ranks on a 1-GPU box
     dev_override = os.environ.get("MYRT_BENCH_DEVICE")
     local = int(dev_override) if dev_override is not None else local
@@ -93,117 +159,79 @@ def main():
 
     cam = scene.cameras[0]
     W, H = cam.image_resolution
-    if args.scaling == "strong" and world > 1:
-        first, step = rank, world          # C4: 8-row chunks dealt round-robin to ranks
-    else:
-        first, step = 0, 1
+    strong = args.scaling == "strong"
+    first, step = (rank, world) if strong else (0, 1)
     rows = M.rows_for_chunks(H, first, step)
-    out = torch.empty((max(rows, 1), W, 3), dtype=torch.float64, device="cuda")
-    stream = torch.cuda.current_stream()
-    sptr = stream.cuda_stream
+    n = int(max(1, cam.num_samples) ** 0.5)
+
+    # ---- the framebuffer the image is delivered into (RGBA8, whole frame, row 0 = top)
+    if strong and world > 1:
+        shared = SharedFrame(W * H * 4, rank, world, dist, args.config)
+        M.register_host(shared.array)
+        fb = shared.array.reshape(H, W, 4)
+    else:
+        shared = None
+        fb = M.pinned_array((H, W, 4), np.uint8)
+        fb[:] = 0
 
     def frame():
-        eng.render_device(out.data_ptr(), 0, first, step, stream=sptr)
+        return eng.render_into(0, first, step, rgb=None, rgba=fb, frame_layout=True)
 
+    st = None
     for _ in range(args.warmup):
-        frame()
-    torch.cuda.synchronize()
-    st = eng.collect_stats()
-    n = int(max(1, cam.num_samples) ** 0.5)
+        st = frame()
+    if st is None:
+        st = frame()
     rays_primary = rows * W * n * n
-    rays_shadow = int(st.shadow_rays)
-    rays_secondary = int(st.secondary_rays)     # reflection rays: reported, not in `value`
-    rays_rank = rays_primary + rays_shadow
+    shadow_cast, shadow_traced = int(st.shadow_rays), int(st.shadow_rays_traced)
+    rays_rank = rays_primary + shadow_traced
 
     # ---- timed region: K frames, barrier + sync on both sides
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    kms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_begin = time.perf_counter()
-    for k in range(args.steps):
-        starts[k].record(stream)
-        frame()
-        ends[k].record(stream)
+    for _ in range(args.steps):
+        kms.append(frame().kernel_ms)
     torch.cuda.synchronize()
     t_elapsed = time.perf_counter() - t_begin
     if world > 1:
         dist.barrier()
-    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+    kernel_ms = statistics.mean(kms)
 
     t_max = t_elapsed
-    rays_total = rays_rank * args.steps
+    tot = np.array([rays_rank, rays_primary + shadow_cast, shadow_cast, shadow_traced], dtype=np.float64) * args.steps
     if world > 1:
         tt = torch.tensor([t_elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
-        rr = torch.tensor([rays_total], dtype=torch.float64)
+        rr = torch.tensor(tot)
         dist.all_reduce(rr, op=dist.ReduceOp.SUM)
-        rays_total = float(rr.item())
-    value = rays_total / t_max / 1e6
+        tot = rr.numpy()
+        km = torch.tensor([kernel_ms], dtype=torch.float64)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kernel_ms = float(km.item())
+    value = tot[0] / t_max / 1e6
     ms_per_step = t_max * 1e3 / args.steps
 
-    # ---- roofline: algorithmic bytes of one launch, counted on the GPU in
-    # the reference's traversal order (rt_render_device_counted; equal to the oracle's tally,
-    # tests/test_gpu_parity.py), divided by the average launch time of the timed frames.
-    wc = eng.work_counters(out.data_ptr(), 0, first, step, stream=sptr)
-    alg_bytes = (56 * wc.ref_node_fetches + 72 * wc.ref_tri_tests + 72 * wc.ref_smooth_hits
-                 + 24 * wc.ref_pixels)
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic, tpath = None, args.traffic_json
-    if tpath == "auto":
-        tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if tpath and os.path.exists(tpath) and world == 1:
-        try:
-            with open(tpath) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": os.path.relpath(tpath, ROOT) if traffic is not None else None,
-                "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes),
-                "alg_bytes_per_ray": round(alg_bytes / max(1, rays_rank), 1),
-                "alg_counts": {"node_fetches": int(wc.ref_node_fetches), "tri_tests": int(wc.ref_tri_tests),
-                               "smooth_hits": int(wc.ref_smooth_hits), "pixels": int(wc.ref_pixels)},
-                "simd_efficiency": {
-                    "closest": round(wc.lane_steps_closest / max(1, 64 * wc.wave_steps_closest), 3),
-                    "shadow": round(wc.lane_steps_shadow / max(1, 64 * wc.wave_steps_shadow), 3)},
-                "executed": {"records_128B": int(wc.records_fetched), "tri_tests": int(wc.tri_tests),
-                             "normal_fetches": int(wc.normal_fetches), "pixels": int(wc.pixels),
-                             "load_bytes": int(128 * wc.records_fetched + 80 * wc.tri_tests
-                                               + 72 * wc.normal_fetches + 24 * wc.pixels)}}
+    # ---- the gathered image: every row delivered (alpha 255 everywhere), and its hash (equal
+    # for every N: the multi-GPU split changes nothing in the image)
+    if world > 1:
+        dist.barrier()
+    gather = None
+    if rank == 0:
+        gather = {"rows_complete": bool(np.all(fb[:, :, 3] == 255)),
+                  "rgba8_sha256": hashlib.sha256(np.ascontiguousarray(fb).tobytes()).hexdigest()}
 
-    # ---- host-buffer path (rt_render: render + D2H of the FP64 framebuffer + host scatter,
-    # batches overlapped with the copies).  Reported next to `value`, never as `value`.
-    host_path = None
-    if not args.no_host_path:
-        try:
-            import numpy as np
-            host_buf = np.zeros((rows, W, 3), dtype=np.float64)        # caller-owned, reused
-            eng.render_rows(0, first, step, False, out=host_buf)        # staging warm-up
-            t_h = time.perf_counter()
-            nh = 5
-            for _ in range(nh):
-                eng.render_rows(0, first, step, False, out=host_buf)
-            ms_h = (time.perf_counter() - t_h) * 1e3 / nh
-            host_path = {"ms_per_frame": round(ms_h, 4), "value": round(rays_rank / (ms_h * 1e-3) / 1e6, 2),
-                         "unit": "Mrays/s", "what": "rt_render wall time incl. D2H of the FP64 RGB framebuffer"}
-            # caller buffer in page-locked memory (rt_host_alloc): rows DMA'd straight into it
-            pin_rgb, _ = eng.alloc_frame(0, first, step, rgba=False)
-            eng.render_rows(0, first, step, False, out=pin_rgb)
-            t_h = time.perf_counter()
-            for _ in range(nh):
-                eng.render_rows(0, first, step, False, out=pin_rgb)
-            ms_p = (time.perf_counter() - t_h) * 1e3 / nh
-            host_path["pinned"] = {"ms_per_frame": round(ms_p, 4), "value": round(rays_rank / (ms_p * 1e-3) / 1e6, 2),
-                                   "what": "same into a page-locked caller buffer (rt_host_alloc): the kernel stores rows into it over PCIe, no copy"}
-            del pin_rgb
-        except Exception as e:  # pragma: no cover
-            log("host path failed:", e)
+    # ---- roofline (profiles/roofline_<config>.json: PMC passes of this build, tools/pmc_roofline.py)
+    roofline = roofline_fields(args, eng, local, first, step, rows, W, kernel_ms, rays_rank, world)
 
-    # ---- CPU baseline (rank 0, N = 1 only): oracle on a bounded sample of the same frame
+    # ---- side paths on this rank's share: FP64 framebuffer delivery, device-only launch
+    side = None
+    if not args.no_side_paths:
+        side = side_paths(eng, first, step, rows, W, H, rays_rank, args)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -212,55 +240,163 @@ def main():
             log("cpu baseline failed:", e)
             cpu = {"value": None, "unit": "Mrays/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 
+    if shared is not None:
+        shared.close(dist)
     if rank == 0:
         line = {
             "metric": "Mrays/s (primary+shadow), 1920x1080 / 1M-tri PLY, at 1/2/4/8 MI355X",
-            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+            "value": round(float(value), 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong" if args.scaling == "strong" else "weak", "vs_baseline": None,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (seeded scene generator; no bunny/assets offline)",
             "config": {"workload": workload, "width": W, "height": H, "spp": max(1, cam.num_samples),
                        "triangles": int(info.triangles),
-                       "partition": (f"8-row chunks round-robin over {world} GPU(s)" if args.scaling == "strong"
-                                     else f"one full frame per GPU per step, {world} GPU(s), no collective"),
-                       "rays_per_frame": int(rays_rank) if world == 1 else None,
-                       "secondary_rays_per_frame": rays_secondary if world == 1 else None},
+                       "partition": (f"one frame per step, 8-row chunks round-robin over {world} GPU(s), "
+                                     "rows stored into one shared page-locked framebuffer" if strong else
+                                     f"one full frame per GPU per step, {world} GPU(s), no collective"),
+                       "delivered": "RGBA8 frame in page-locked host memory (RayTracerEngine.render's image)"},
+            "rays": {"per_step": int(tot[0] / args.steps), "primary_per_step": int(rays_primary) if world == 1 else None,
+                     "shadow_traced_per_step": int(tot[3] / args.steps),
+                     "shadow_cast_per_step": int(tot[2] / args.steps),
+                     "value_reference_count": round(float(tot[1] / t_max / 1e6), 2),
+                     "note": "value counts shadow rays actually traversed; shadow_cast adds the rays the "
+                             "reference casts where N.L <= 0 and discards (value_reference_count)",
+                     "secondary_per_step": int(st.secondary_rays) if world == 1 else None},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "host_path": host_path,
+            "gather": gather,
+            "side_paths": side,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
+def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, world):
+    import torch
+    out = torch.empty((max(rows, 1), W, 3), dtype=torch.float64, device=f"cuda:{dev}")
+    wc = eng.work_counters(out.data_ptr(), 0, first, step, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    del out
+    alg_bytes = (56 * wc.ref_node_fetches + 72 * wc.ref_tri_tests + 72 * wc.ref_smooth_hits + 24 * wc.ref_pixels)
+    load_bytes = 128 * wc.records_fetched + 80 * wc.tri_tests + 72 * wc.normal_fetches + 24 * wc.pixels
+    prof, ppath = None, args.profile_json
+    if ppath == "auto":
+        ppath = os.path.join(ROOT, "profiles", f"roofline_{args.config}.json")
+    if ppath and os.path.exists(ppath):
+        with open(ppath) as fh:
+            prof = json.load(fh)
+    lib_sha = _lib_sha()
+    r = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+         "kernel_ms": round(kernel_ms, 4),
+         "kernel_ms_source": "HIP events around the render launch on its stream, inside rt_render, timed steps"}
+    if prof is not None and world == 1:
+        traffic = prof["hbm_bytes_per_launch"]
+        r["traffic"] = int(traffic)
+        r["achieved"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 2)
+        r["frac"] = round(r["achieved"] / HBM_PEAK_GBS, 4)
+        r["traffic_source"] = os.path.relpath(ppath, ROOT)
+        r["profile_build_matches"] = prof.get("lib_sha256_16") == lib_sha
+        r["binding"] = {
+            "resource": "vector-memory data path (TA/TD): per-lane BVH record and triangle loads served from L1/L2",
+            "td_busy": prof.get("td_busy"), "ta_busy": prof.get("ta_busy"),
+            "valu_lane_util": prof.get("valu_lane_util"),
+            "note": "td_busy = TD_TD_BUSY_sum/256 / (GRBM_GUI_ACTIVE/8) from the same profile",
+            "executed_load_bytes": int(load_bytes),
+            "executed_load_GBs": round(load_bytes / (kernel_ms * 1e-3) / 1e9, 1)}
+    r["reference_work"] = {
+        "what": "SURVEY.md 8(d) algorithmic bytes of the reference's unpruned walk (56 N_node + 72 N_tri + "
+                "72 N_smooth + 24 N_px), counted on the GPU in reference order; most are cache hits, so the "
+                "equivalent rate exceeds HBM peak and is NOT an HBM fraction",
+        "bytes_per_launch": int(alg_bytes), "bytes_per_ray": round(alg_bytes / max(1, rays_rank), 1),
+        "equiv_GBs": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 1),
+        "counts": {"node_fetches": int(wc.ref_node_fetches), "tri_tests": int(wc.ref_tri_tests),
+                   "smooth_hits": int(wc.ref_smooth_hits), "pixels": int(wc.ref_pixels)}}
+    r["executed"] = {"records": int(wc.records_fetched), "tri_tests": int(wc.tri_tests),
+                     "normal_fetches": int(wc.normal_fetches), "pixels": int(wc.pixels)}
+    r["simd_efficiency"] = {"closest": round(wc.lane_steps_closest / max(1, 64 * wc.wave_steps_closest), 3),
+                            "shadow": round(wc.lane_steps_shadow / max(1, 64 * wc.wave_steps_shadow), 3)}
+    r["lib_sha256_16"] = lib_sha
+    return r
+
+
+def _lib_sha():
+    from myraytracer_amd.engine import LIB_PATH
+    path = os.environ.get("MYRT_LIB") or LIB_PATH
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def side_paths(eng, first, step, rows, W, H, rays_rank, args):
+    """FP64 [Vec3] frame (Renderer.render's output) delivered to page-locked host memory, and
+    the launch alone with the image left in HBM (no delivery)."""
+    import numpy as np
+    import torch
+    import myraytracer_amd as M
+    res = {}
+    rgb = M.pinned_array((H, W, 3), np.float64)
+    eng.render_into(0, first, step, rgb=rgb, rgba=None, frame_layout=True)
+    nh = 10
+    t = time.perf_counter()
+    for _ in range(nh):
+        eng.render_into(0, first, step, rgb=rgb, rgba=None, frame_layout=True)
+    ms = (time.perf_counter() - t) * 1e3 / nh
+    res["fp64_path"] = {"ms_per_frame": round(ms, 4), "value": round(rays_rank / (ms * 1e-3) / 1e6, 2),
+                        "what": "rt_render of the FP64 RGB framebuffer (24 B/px) into page-locked host memory"}
+    del rgb
+    out = torch.empty((max(rows, 1), W, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    for _ in range(3):
+        eng.render_device(0, 0, first, step, stream=stream.cuda_stream, out_rgba_ptr=out.data_ptr())
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(20):
+        eng.render_device(0, 0, first, step, stream=stream.cuda_stream, out_rgba_ptr=out.data_ptr())
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) * 1e3 / 20
+    res["device_only"] = {"ms_per_frame": round(ms, 4), "value": round(rays_rank / (ms * 1e-3) / 1e6, 2),
+                          "what": "rt_render_device back to back, RGBA8 left in HBM (no delivery)"}
+    return res
+
+
+def cpu_threads(args):
+    if args.cpu_threads:
+        return args.cpu_threads
+    share = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")          # the pool's CPU share per GPU (16 on the box)
+    if omp and omp.isdigit():
+        share = min(share, int(omp))
+    return max(1, share)
+
+
 def cpu_baseline(scene, H, args):
-    """Oracle (C++ restatement of the reference CPU renderer) on every k-th 8-row chunk."""
+    """Oracle (C++ restatement of the reference CPU renderer): median over whole frames at the
+    CPU share (one task per 8-row chunk, Object+Extension.swift:285-360), plus 1 thread."""
     import oracle
-    cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    cores = cpu_threads(args)
     t0 = time.time()
     o = oracle.OracleScene(scene if scene.objects[0].ply_path is None else _inline(scene))
     build_s = time.time() - t0
     nchunks = (H + 7) // 8
-    # calibrate on one chunk, then size the sample to ~cpu_seconds of wall time: a strided
-    # subset of the frame's 8-row chunks, or whole frames repeated when one frame is shorter
-    _, st = o.render(0, nchunks // 2, nchunks, threads=1)
-    per_chunk_s = max(st.milliseconds / 1e3, 1e-4)
-    want = max(1, int(args.cpu_seconds * cores / per_chunk_s))
-    stride = max(1, nchunks // want)
-    frames = max(1, min(50, int(want // nchunks))) if stride == 1 else 1
-    rays = 0
-    ms = 0.0
-    px = 0
-    for _ in range(frames):
-        _, st = o.render(0, 0, stride, threads=cores)
-        rays += st.primary_rays + st.shadow_rays
-        ms += st.milliseconds
-        px += st.pixels
-    what = (f"{frames} full frame(s)" if stride == 1 else f"every {stride}th 8-row chunk of the frame")
-    return {"value": round(rays / (ms / 1e3) / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"{what} ({px} px, {rays} rays, {ms / 1e3:.1f}s on {cores} threads; "
-                      f"oracle BVH build {build_s:.1f}s excluded)"}
+    rates, px = [], 0
+    for _ in range(max(1, args.cpu_frames)):
+        _, st = o.render(0, 0, 1, threads=cores)
+        rates.append((st.primary_rays + st.shadow_rays) / (st.milliseconds / 1e3) / 1e6)
+        px = st.pixels
+    stride = 16
+    one = []
+    for k in range(2):
+        _, st = o.render(0, k, stride, threads=1)
+        one.append((st.primary_rays + st.shadow_rays) / (st.milliseconds / 1e3) / 1e6)
+    med = statistics.median(rates)
+    return {"value": round(med, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "frames": [round(x, 3) for x in rates], "spread": round((max(rates) - min(rates)) / med, 3),
+            "one_thread": round(statistics.median(one), 4),
+            "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "sample": f"median of {len(rates)} whole frames ({px} px each) on {cores} threads (the GPU box's "
+                      f"CPU share: OMP_NUM_THREADS; nproc reports the whole machine); one_thread = every "
+                      f"{stride}th 8-row chunk on 1 thread, {len(one)} runs; rays = primary + shadow cast; "
+                      f"oracle BVH build {build_s:.1f}s excluded"}
 
 
 def _inline(scene):

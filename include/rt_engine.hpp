@@ -64,6 +64,7 @@ struct RenderStats {                                    /* Models/RenderStats.sw
     int64_t meshes = 0, triangles = 0, spheres = 0, planes = 0;
     int64_t rays = 0;                                   /* primary + shadow */
     int64_t primary_rays = 0, shadow_rays = 0, secondary_rays = 0;
+    int64_t shadow_rays_traced = 0;                     /* any-hit walks that ran (<= shadow_rays) */
     double milliseconds = 0, kernel_ms = 0;
 };
 
@@ -161,6 +162,7 @@ public:
         r.stats.secondary_rays = st.secondary_rays;
         r.stats.rays = st.primary_rays + st.shadow_rays;
         r.stats.milliseconds = st.milliseconds; r.stats.kernel_ms = st.kernel_ms;
+        r.stats.shadow_rays_traced = st.shadow_rays_traced;
         return r;
     }
 

@@ -114,12 +114,14 @@ typedef struct rt_object {
     const char*    ply_path;
     const double*  positions;   int64_t num_positions;   /* xyz triples               */
     const int32_t* indices;     int64_t num_indices;     /* triangle list             */
-    const double*  normals;     /* optional per-vertex normals (PLY branch, RTContext.swift:267-297) */
+    const double*  normals;     /* optional per-vertex normals (PLY branch, RTContext.swift:267-297);
+                                 * length in num_normals below                            */
     /* analytic payloads (RT_OBJ_TRIANGLE / SPHERE / PLANE)                           */
     rt_vec3 v[3];               /* triangle vertices                                   */
     rt_vec3 center;             /* sphere / plane center                               */
     rt_vec3 normal;             /* plane normal                                        */
     double  radius;             /* sphere radius                                       */
+    int64_t num_normals;        /* xyz triples behind `normals`; must equal num_positions */
 } rt_object;
 
 typedef struct rt_scene_desc {
@@ -148,6 +150,9 @@ typedef struct rt_stats {       /* RenderStats (Models/RenderStats.swift:8-24) +
     int64_t secondary_rays;     /* reflection rays                                     */
     double  milliseconds;       /* wall time of the render call                        */
     double  kernel_ms;          /* device time of the render kernels                   */
+    int64_t shadow_rays_traced; /* shadow rays whose any-hit walk actually ran: the walk is
+                                 * skipped when !(N.L > 0), where the reference discards the
+                                 * occlusion result (Object+Extension.swift:123-141)      */
 } rt_stats;
 
 typedef struct rt_scene_info {
@@ -184,12 +189,26 @@ int32_t rt_render(rt_scene* scene, int32_t camera_index, int32_t chunk_first, in
                   double* out_rgb, uint8_t* out_rgba8, rt_stats* stats,
                   rt_progress_fn progress, void* user);
 
-/* Page-locked host buffers for rt_render outputs (hipHostMalloc).  When out_rgb /
- * out_rgba8 lie inside one such allocation (or in memory the caller registered with
- * hipHostRegister), rt_render DMAs finished rows straight into them instead of going
- * through its own pinned staging and a host memcpy.  Any other host memory still works. */
+/* rt_render with flags.  RT_RENDER_FRAME_LAYOUT: out_rgb / out_rgba8 are whole W x H
+ * frames (W*H*3 doubles / W*H*4 bytes) and the selected chunks' rows are written at
+ * their image rows; other rows are left untouched.  Several renders of disjoint chunk
+ * selections (other devices, other processes sharing one registered buffer) thereby
+ * gather one image with no copy.  rt_render(...) == rt_render_ex(..., 0, ...). */
+#define RT_RENDER_FRAME_LAYOUT  1u
+int32_t rt_render_ex(rt_scene* scene, int32_t camera_index, int32_t chunk_first, int32_t chunk_step,
+                     double* out_rgb, uint8_t* out_rgba8, uint32_t flags, rt_stats* stats,
+                     rt_progress_fn progress, void* user);
+
+/* Page-locked host buffers for rt_render outputs (hipHostMalloc, mapped + portable).
+ * When out_rgb / out_rgba8 lie inside one such allocation (or a range registered with
+ * rt_host_register), the render kernels of every device replica store their rows
+ * straight into them over PCIe; other host memory goes through pinned staging and a
+ * host memcpy.  rt_host_register pins existing host memory (e.g. a shared-memory
+ * framebuffer mapped by several processes); unregister before unmapping it. */
 int32_t rt_host_alloc(uint64_t bytes, void** out);
 void    rt_host_free(void* ptr);
+int32_t rt_host_register(void* ptr, uint64_t bytes);
+int32_t rt_host_unregister(void* ptr);
 
 /* Same as rt_render on ONE device slot, but outputs are DEVICE pointers on that
  * device and the work is enqueued on `stream` (a hipStream_t, NULL = default)

@@ -11,9 +11,10 @@ from .scene import (AreaLight, Camera, Material, Mesh, MeshInstance, Plane, Poin
                     Triangle, translation)
 from .sceneio import SceneLoadError, load as load_scene, loads as loads_scene, save_png  # noqa: F401
 from .engine import (CameraSpec, RayTracerEngine, RenderError, RenderProgress, RenderResult,  # noqa: F401
-                     RenderStats, SceneInfo, load_library, ply_load, rows_for_chunks)
+                     RenderStats, SceneInfo, load_library, pinned_array, ply_load, register_host,
+                     rows_for_chunks, unregister_host)
 
 __all__ = ["RayTracerEngine", "Scene", "Camera", "Material", "Mesh", "MeshInstance", "Triangle", "Sphere", "Plane",
            "PointLight", "AreaLight", "RenderResult", "RenderStats", "RenderProgress", "RenderError", "SceneInfo",
            "CameraSpec", "load_library", "ply_load", "rows_for_chunks", "translation", "load_scene", "loads_scene",
-           "save_png", "SceneLoadError"]
+           "save_png", "SceneLoadError", "pinned_array", "register_host", "unregister_host"]

@@ -45,7 +45,8 @@ class rt_object(C.Structure):
                 ("positions", c_double_p), ("num_positions", C.c_int64),
                 ("indices", c_int32_p), ("num_indices", C.c_int64),
                 ("normals", c_double_p),
-                ("v", rt_vec3 * 3), ("center", rt_vec3), ("normal", rt_vec3), ("radius", C.c_double)]
+                ("v", rt_vec3 * 3), ("center", rt_vec3), ("normal", rt_vec3), ("radius", C.c_double),
+                ("num_normals", C.c_int64)]
 
 
 class rt_scene_desc(C.Structure):
@@ -59,10 +60,14 @@ class rt_scene_desc(C.Structure):
                 ("objects", C.POINTER(rt_object)), ("cameras", C.POINTER(rt_camera))]
 
 
+RT_RENDER_FRAME_LAYOUT = 1
+
+
 class rt_stats(C.Structure):
     _fields_ = [("meshes", C.c_int64), ("triangles", C.c_int64), ("spheres", C.c_int64), ("planes", C.c_int64),
                 ("primary_rays", C.c_int64), ("shadow_rays", C.c_int64), ("secondary_rays", C.c_int64),
-                ("milliseconds", C.c_double), ("kernel_ms", C.c_double)]
+                ("milliseconds", C.c_double), ("kernel_ms", C.c_double),
+                ("shadow_rays_traced", C.c_int64)]
 
 
 class rt_scene_info(C.Structure):
@@ -113,6 +118,7 @@ EXPORTED_SYMBOLS = [
     "rt_stats_collect", "rt_rows_for_chunks", "rt_render_device_counted", "rt_last_error", "rt_version",
     "rt_ply_load", "rt_ply_free", "rt_debug_bvh_hash", "rt_debug_host_build",
     "rt_debug_trace_rays", "rt_debug_occluded_rays", "rt_host_alloc", "rt_host_free", "rt_debug_wave_times",
+    "rt_render_ex", "rt_host_register", "rt_host_unregister",
 ]
 
 
@@ -128,6 +134,13 @@ def bind(lib: C.CDLL) -> C.CDLL:
     lib.rt_render.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, c_double_p, P(C.c_uint8),
                               P(rt_stats), RT_PROGRESS_FN, C.c_void_p]
     lib.rt_render.restype = C.c_int32
+    lib.rt_render_ex.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, c_double_p, P(C.c_uint8),
+                                 C.c_uint32, P(rt_stats), RT_PROGRESS_FN, C.c_void_p]
+    lib.rt_render_ex.restype = C.c_int32
+    lib.rt_host_register.argtypes = [C.c_void_p, C.c_uint64]
+    lib.rt_host_register.restype = C.c_int32
+    lib.rt_host_unregister.argtypes = [C.c_void_p]
+    lib.rt_host_unregister.restype = C.c_int32
     lib.rt_render_device.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                      C.c_void_p, C.c_void_p]
     lib.rt_render_device.restype = C.c_int32

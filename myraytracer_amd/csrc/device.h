@@ -103,6 +103,11 @@ struct PCG32 {
 // while every XCD still samples the whole image (whole-band splits are badly
 // imbalanced: sky rows cost a fraction of terrain rows).  Bijective on [0, nb): the
 // tail beyond the last full 8*G round keeps identity order.
+// Output row of chunk `chunk`, row `r` (RenderParams::out_first / out_step).
+__device__ __forceinline__ size_t out_row_of(const RenderParams& P, int chunk, int r) {
+    return (size_t)((chunk - P.out_first) / P.out_step) * 8 + (size_t)r;
+}
+
 __device__ __forceinline__ int xcd_tile(int b, int nb, int G) {
     if (G <= 1) return b;
     const int round = 8 * G, full = nb / round * round;
@@ -128,7 +133,8 @@ constexpr int kLds = MYRT_KLDS;
 #ifndef MYRT_STRIDE64
 #define MYRT_STRIDE64 1      // per-wave LDS slab with a constant stride of 64 (shift, not multiply)
 #endif
-constexpr int kSpill = 64;
+constexpr int kSpill = kStackCap - kLds;   // the host refuses deeper scenes (scene.cpp, RT_ERR_STACK)
+static_assert(kSpill > 0, "LDS part larger than the stack");
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 typedef __attribute__((address_space(5))) unsigned long long priv_u64;
 struct Stack {
@@ -203,6 +209,7 @@ struct Counts {
     unsigned shadow, secondary;
     unsigned long long recs, tris, normals, insts, nodes, smooth;
     unsigned long long it_closest, it_shadow;   // loop iterations of this lane (divergence study)
+    unsigned shadow_traced;                     // shadow rays whose any-hit walk ran (<= shadow)
 };
 constexpr int kMissRef = 0x7fffffff;   // count_ref any-hit: a pushed child whose slab test missed
 

@@ -128,6 +128,10 @@ struct RenderParams {
     double background[3], ambient[3];
     int32_t max_depth;
     int32_t chunk_first, chunk_step, num_chunks;   // selected 8-row chunks
+    // output row of chunk c, row r: ((c - out_first) / out_step) * 8 + r.  Packed selection
+    // rows: out_first = chunk_first, out_step = chunk_step; full-frame layout (rows at their
+    // image positions, RT_RENDER_FRAME_LAYOUT): out_first = 0, out_step = 1.
+    int32_t out_first, out_step;
     int32_t stack_depth;             // LDS stack entries per lane
     int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
@@ -142,11 +146,18 @@ struct RenderParams {
     int32_t has_special;             // spheres / planes present (general walk tests kinds)
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
-    unsigned long long* counters;    // [0] shadow rays, [1] secondary rays, [2..8] work counters (kCounterWords)
+    unsigned long long* counters;    // [0] shadow rays cast, [1] secondary rays, [2..12] work counters,
+                                     // [13] shadow rays traversed (kCounterWords)
     unsigned long long* wave_times;  // debug (rt_debug_wave_times): per wave {start, end, tile} in 100 MHz ticks
 };
 
 constexpr int kCounterWords = 16;   // u64 words behind RenderParams::counters
+constexpr int kCounterShadowTraced = 13;
 constexpr int kMaxDepthGPU = 16;     // mirror/conductor recursion levels kept per lane
+
+// Per-lane traversal stack capacity (device.h Stack: kLds LDS entries + the private rest).
+// The reference gives the TLAS walk and each BLAS walk their own 64-entry stacks
+// (RTContext.swift:550, 623); one shared stack of 128 holds both at their limits.
+constexpr int kStackCap = 128;
 
 }  // namespace myrt

@@ -83,6 +83,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                     contrib = (Ld + Ls) * atten;
                 }
                 if (NdotL > 0 || MYRT_REF(P)) {
+                    c.shadow_traced++;
                     const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
                                              : occluded<COUNT>(P, so, wi, dist, time, st, c);
                     if (!blocked && NdotL > 0) Lo = Lo + contrib;
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     const int j = chunk * 8 + rowInChunk;
     const DCamera& C = P.cam;
     const bool valid = (i < C.width) && (j < C.height);
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{};
     if (valid) {
         MYRT_STACK(st, lds_stack);
         PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             }
         }
         const V3 px = pixel / (double)C.samples;
-        const size_t row = (size_t)slot * 8 + rowInChunk;
+        const size_t row = out_row_of(P, chunk, rowInChunk);
         const size_t o = row * (size_t)C.width + i;
         if (P.out_rgb) {
             P.out_rgb[o * 3 + 0] = px.x;
@@ -241,10 +242,12 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     }
 #endif
     // ray / work counters: one atomic per wave
-    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary);
+    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
+                             s2 = wave_sum(cnt.shadow_traced);
     if (lane == 0) {
         if (s0) atomicAdd(&P.counters[0], s0);
         if (s1) atomicAdd(&P.counters[1], s1);
+        if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
     }
     if (COUNT) {
         const unsigned long long a = wave_sum(cnt.recs), b = wave_sum(cnt.tris), cc = wave_sum(cnt.normals),
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(256) void k_trace_rays(RenderParams P, RayBatch B) 
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B.n) return;
     MYRT_STACK(st, lds_stack);
-    Counts c{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts c{};
     const V3 o = v3(B.o[3 * i], B.o[3 * i + 1], B.o[3 * i + 2]), d = v3(B.d[3 * i], B.d[3 * i + 1], B.d[3 * i + 2]);
     const double time = B.time[i];
     Hit h;
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(256) void k_occluded_rays(RenderParams P, RayBatch 
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B.n) return;
     MYRT_STACK(st, lds_stack);
-    Counts c{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts c{};
     const V3 o = v3(B.o[3 * i], B.o[3 * i + 1], B.o[3 * i + 2]), d = v3(B.d[3 * i], B.d[3 * i + 1], B.d[3 * i + 2]);
     const bool hit = B.uni ? uni_occluded<false>(P, o, d, B.tlim[i], st, c)
                            : occluded<false>(P, o, d, B.tlim[i], B.time[i], st, c);
@@ -510,6 +513,22 @@ extern "C" int32_t rt_rows_for_chunks(int32_t height, int32_t chunk_first, int32
     return rows;
 }
 
+// Absolute pruning margin for rays whose origins lie within `origin_dist` of the scene
+// center (or inside the scene bounds): prune_k * (|o - v0| + t|d|) with both terms bounded
+// by the origin's distance plus the scene diagonal (scene.cpp, "pruning margin").
+static double prune_abs_for(const HostScene& S, double origin_dist) {
+    const double half = 0.5 * S.scene_extent;
+    const double rmax = std::max(origin_dist, half) + half + S.max_motion;
+    const double mt = 2.0 * S.prune_k * (2.0 * rmax + S.scene_extent);
+    const double a = std::max(1e-9 * S.scene_extent, mt);
+    return std::isfinite(a) ? a : HUGE_VAL;                          // eps <= 0: no pruning
+}
+static double dist_to_center(const HostScene& S, const double p[3]) {
+    double d = 0.0;
+    for (int k = 0; k < 3; ++k) d += (p[k] - S.scene_center[k]) * (p[k] - S.scene_center[k]);
+    return std::sqrt(d);
+}
+
 static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32_t cam, int32_t first, int32_t step,
                                 double* out_rgb, uint8_t* out_rgba8) {
     const HostScene& S = s->host;
@@ -525,8 +544,16 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.num_plights = (int32_t)S.plights.size();
     P.cam = camera_constants(S.cams[cam]);
     P.eps = S.eps; P.shadow_eps = S.shadow_eps;
+    // Pruning margin (DESIGN.md "Pruning", scene.cpp): relative 1e-7 covers the rounding of
+    // slab entries and sphere roots; the absolute part bounds Moeller-Trumbore's t error,
+    // prune_k * (|o - v0| + t|d|), for every ray origin of this render: the camera (plus the
+    // lens) or a hit point inside the scene bounds.
     P.prune_rel = 1.0 + 1e-7;
-    P.prune_abs = 1e-9 * S.scene_extent;
+    {
+        const rt_camera& cam0 = S.cams[cam];
+        const double ce[3] = {cam0.position.x, cam0.position.y, cam0.position.z};
+        P.prune_abs = prune_abs_for(S, dist_to_center(S, ce) + std::fabs(cam0.aperture_size));
+    }
     {   // FP32-enclosed slabs (slab32.h): eps rounded out, and a bound on every coordinate of an
         // identity scene (every box of the unified walk lies inside the TLAS root box)
         P.eps_up32 = f32slab::up(P.eps);
@@ -541,6 +568,7 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     for (int k = 0; k < 3; ++k) { P.background[k] = S.background[k]; P.ambient[k] = S.ambient[k]; }
     P.max_depth = S.max_depth;
     P.chunk_first = first; P.chunk_step = step;
+    P.out_first = first; P.out_step = step;          // packed selection rows (callers may remap)
     int32_t nsel = 0;
     for (int32_t c = first; c < num_chunks_total(P.cam.height); c += step) nsel++;
     P.num_chunks = nsel;
@@ -752,7 +780,10 @@ int32_t rt_stats_collect(rt_scene* s, int32_t slot, rt_stats* stats) {
     HIP_TRY(hipSetDevice(r.device));
     unsigned long long c[kCounterWords];
     HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
-    if (stats) { stats->shadow_rays = (int64_t)c[0]; stats->secondary_rays = (int64_t)c[1]; }
+    if (stats) {
+        stats->shadow_rays = (int64_t)c[0]; stats->secondary_rays = (int64_t)c[1];
+        stats->shadow_rays_traced = (int64_t)c[kCounterShadowTraced];
+    }
     return RT_OK;
 }
 
@@ -819,7 +850,7 @@ int32_t rt_host_alloc(uint64_t bytes, void** out) {
     if (!out) return fail(RT_ERR_INVALID_ARG, "null output pointer");
     *out = nullptr;
     if (bytes == 0) return RT_OK;
-    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(out, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
         (void)hipGetLastError();
         *out = nullptr;
         return fail(RT_ERR_OOM, "hipHostMalloc failed");
@@ -834,38 +865,50 @@ void rt_host_free(void* ptr) {
 
 // Host-buffer render across all device replicas (Renderer.render + renderRGBA8Async,
 // Object+Extension.swift:52-379, RayTracer.swift:137-205).  Chunk k of the selection goes to
-// replica (k mod D).  Each replica renders its chunks in up to kRenderBatches launches on its
-// compute stream while a copy stream moves finished batches into pinned staging, so PCIe
-// transfer overlaps rendering; the calling thread scatters finished rows into the caller's
-// buffer, reports progress after every batch and honours cancellation at batch granularity
-// (the reference's cancel was a no-op).  No collective is involved.
-int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb, uint8_t* out_rgba8,
-                  rt_stats* stats, rt_progress_fn progress, void* user) {
+// replica (k mod D).  Outputs in page-locked memory (rt_host_alloc / rt_host_register) are
+// written by the kernels themselves over PCIe (host-mapped, no copy); other host memory is
+// filled from batches that render on the compute stream while a copy stream moves the
+// previous batch into pinned staging and the calling thread scatters it.  Progress is
+// reported after every batch and cancellation is honoured at batch granularity (SURVEY.md
+// §8b; the reference's cancel was a no-op).  No collective is involved.
+// flags & RT_RENDER_FRAME_LAYOUT: outputs are whole W x H frames and the selected chunks'
+// rows land at their image rows (several processes can fill disjoint rows of one shared
+// framebuffer: bench.py's multi-GPU gather).
+int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb, uint8_t* out_rgba8,
+                     uint32_t flags, rt_stats* stats, rt_progress_fn progress, void* user) {
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
     if (s->devs.empty()) return fail(RT_ERR_NO_RENDERER, "Renderer not initialized.");
     if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
+    if (flags & ~(uint32_t)RT_RENDER_FRAME_LAYOUT) return fail(RT_ERR_INVALID_ARG, "unknown render flags");
     int32_t rc = check_renderable(s->host, cam);
     if (rc != RT_OK) return rc;
     std::lock_guard<std::mutex> lock(s->mu);
     auto t0 = std::chrono::steady_clock::now();
     const rt_camera& C = s->host.cams[cam];
     const int32_t W = std::max(1, C.width), H = std::max(1, C.height);
+    const bool frame = (flags & RT_RENDER_FRAME_LAYOUT) != 0;
     std::vector<int32_t> sel;
     for (int32_t c = first; c < num_chunks_total(H); c += step) sel.push_back(c);
     const int32_t D = (int32_t)s->devs.size();
+    // output row of selection entry e: packed (rowOff) or its image row (frame layout)
     std::vector<int32_t> rowOff(sel.size() + 1, 0);
     for (size_t q = 0; q < sel.size(); ++q) rowOff[q + 1] = rowOff[q] + std::min(8, H - 8 * sel[q]);
     const int32_t rowsTotal = rowOff.back();
-    // outputs in page-locked memory: finished rows are DMA'd straight into the caller's
-    // buffer (coalesced per run of adjacent chunks) and the host scatter disappears
-    const bool direct = pinned_range(out_rgb, (size_t)rowsTotal * W * 3 * sizeof(double)) &&
-                        pinned_range(out_rgba8, (size_t)rowsTotal * W * 4);
-    // one replica writing a pinned caller buffer: the kernels store rows straight into it
-    // over PCIe (host-mapped) while they render, with no copy at all
-    double* zc_rgb = nullptr; uint8_t* zc_rgba = nullptr;
-    const bool zerocopy = direct && D == 1 && env_int("MYRT_ZEROCOPY", 1, 0, 1) == 1 &&
-        (!out_rgb || hipHostGetDevicePointer((void**)&zc_rgb, out_rgb, 0) == hipSuccess) &&
-        (!out_rgba8 || hipHostGetDevicePointer((void**)&zc_rgba, out_rgba8, 0) == hipSuccess);
+    auto dstRow = [&](size_t e) -> int32_t { return frame ? 8 * sel[e] : rowOff[e]; };
+    const int32_t outRows = frame ? H : rowsTotal;
+    // outputs in page-locked memory: finished rows go straight into the caller's buffer
+    const bool direct = pinned_range(out_rgb, (size_t)outRows * W * 3 * sizeof(double)) &&
+                        pinned_range(out_rgba8, (size_t)outRows * W * 4);
+    // ... and the kernels can store them there themselves (host-mapped), for any number of
+    // replicas: each maps the buffer and writes its own chunks' rows
+    std::vector<double*> zc_rgb(D, nullptr);
+    std::vector<uint8_t*> zc_rgba(D, nullptr);
+    bool zerocopy = direct && env_int("MYRT_ZEROCOPY", 1, 0, 1) == 1;
+    for (int32_t k = 0; k < D && zerocopy; ++k) {
+        HIP_TRY(hipSetDevice(s->devs[k].device));
+        zerocopy = (!out_rgb || hipHostGetDevicePointer((void**)&zc_rgb[k], out_rgb, 0) == hipSuccess) &&
+                   (!out_rgba8 || hipHostGetDevicePointer((void**)&zc_rgba[k], out_rgba8, 0) == hipSuccess);
+    }
     (void)hipGetLastError();
     // Launches per replica.  Each batch ends on its slowest tile, so batches cost time
     // (~0.1-0.2 ms each on C3): they are used for progress granularity when a callback is
@@ -895,13 +938,13 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
         }
         HIP_TRY(hipSetDevice(r.device));
         const int64_t px = (int64_t)pl.rows * W;
-        if (px > r.out_cap_px) {
+        if (!zerocopy && px > r.out_cap_px) {
             (void)hipFree(r.out_d); (void)hipFree(r.out8_d); r.out_d = nullptr; r.out8_d = nullptr; r.out_cap_px = 0;
             HIP_TRY(hipMalloc((void**)&r.out_d, px * 3 * sizeof(double)));
             HIP_TRY(hipMalloc((void**)&r.out8_d, px * 4));
             r.out_cap_px = px;
         }
-        if (px > r.host_cap_px) {
+        if (!direct && px > r.host_cap_px) {
             if (r.host_rgb) (void)hipHostFree(r.host_rgb);
             if (r.host_rgba) (void)hipHostFree(r.host_rgba);
             r.host_rgb = nullptr; r.host_rgba = nullptr; r.host_cap_px = 0;
@@ -924,10 +967,21 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
             HIP_TRY(hipSetDevice(r.device));
             const int32_t c0 = pl.myFirst + b * pl.per * pl.myStep;
             const int32_t nc = std::min(pl.per, pl.nChunks - b * pl.per);
-            double* drgb = (zerocopy && zc_rgb ? zc_rgb : r.out_d) + (size_t)pl.batchRow[b] * W * 3;
-            uint8_t* drgba = out_rgba8 ? (zerocopy ? zc_rgba : r.out8_d) + (size_t)pl.batchRow[b] * W * 4 : nullptr;
+            double* drgb;
+            uint8_t* drgba;
+            if (zerocopy) {          // the caller's buffer, addressed by the global row mapping
+                drgb = zc_rgb[k];
+                drgba = zc_rgba[k];
+            } else {                 // this batch's rows, packed, in device staging
+                drgb = out_rgb ? r.out_d + (size_t)pl.batchRow[b] * W * 3 : nullptr;
+                drgba = out_rgba8 ? r.out8_d + (size_t)pl.batchRow[b] * W * 4 : nullptr;
+            }
             RenderParams P = make_params(s, r, cam, c0, pl.myStep, drgb, drgba);
             P.num_chunks = nc;
+            if (zerocopy) {
+                P.out_first = frame ? 0 : first;
+                P.out_step = frame ? 1 : step;
+            }
             const int32_t lrc = launch(s, r, P, r.stream, false);
             if (lrc != RT_OK) return lrc;
             HIP_TRY(hipEventRecord(r.batch_done[b], r.stream));
@@ -939,7 +993,7 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
             HIP_TRY(hipStreamWaitEvent(r.copy_stream, r.batch_done[b], 0));
             if (direct) {
                 // replica k's q-th chunk is selection entry k + q*D; its rows follow the
-                // batch's earlier chunks in drgb
+                // batch's earlier chunks in drgb.  Runs of adjacent output rows are one copy.
                 int32_t q = b * pl.per;
                 const int32_t qEnd = q + nc;
                 size_t srcRow = 0;
@@ -947,25 +1001,27 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
                     const size_t e0 = (size_t)k + (size_t)q * D;
                     int32_t nr = rowOff[e0 + 1] - rowOff[e0];
                     int32_t q1 = q + 1;
-                    while (q1 < qEnd) {                     // extend over adjacent output rows
+                    while (q1 < qEnd) {
                         const size_t e = (size_t)k + (size_t)q1 * D;
-                        if (rowOff[e] != rowOff[e0] + nr) break;
+                        if (dstRow(e) != dstRow(e0) + nr) break;
                         nr += rowOff[e + 1] - rowOff[e];
                         ++q1;
                     }
+                    const size_t d0 = (size_t)dstRow(e0);
                     if (out_rgb)
-                        HIP_TRY(hipMemcpyAsync(out_rgb + (size_t)rowOff[e0] * W * 3, drgb + srcRow * W * 3,
+                        HIP_TRY(hipMemcpyAsync(out_rgb + d0 * W * 3, drgb + srcRow * W * 3,
                                                (size_t)nr * W * 3 * sizeof(double), hipMemcpyDeviceToHost,
                                                r.copy_stream));
                     if (out_rgba8)
-                        HIP_TRY(hipMemcpyAsync(out_rgba8 + (size_t)rowOff[e0] * W * 4, drgba + srcRow * W * 4,
+                        HIP_TRY(hipMemcpyAsync(out_rgba8 + d0 * W * 4, drgba + srcRow * W * 4,
                                                (size_t)nr * W * 4, hipMemcpyDeviceToHost, r.copy_stream));
                     srcRow += (size_t)nr;
                     q = q1;
                 }
             } else {
-                HIP_TRY(hipMemcpyAsync(r.host_rgb + (size_t)pl.batchRow[b] * W * 3, drgb,
-                                       nrows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, r.copy_stream));
+                if (out_rgb)
+                    HIP_TRY(hipMemcpyAsync(r.host_rgb + (size_t)pl.batchRow[b] * W * 3, drgb,
+                                           nrows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, r.copy_stream));
                 if (out_rgba8)
                     HIP_TRY(hipMemcpyAsync(r.host_rgba + (size_t)pl.batchRow[b] * W * 4, drgba, nrows * W * 4,
                                            hipMemcpyDeviceToHost, r.copy_stream));
@@ -1009,9 +1065,10 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
                     const size_t e = (size_t)k + (size_t)q * D;
                     const int32_t nr = rowOff[e + 1] - rowOff[e];
                     const int32_t sr = src[q - q0];
-                    if (out_rgb) std::memcpy(out_rgb + (size_t)rowOff[e] * W * 3, r.host_rgb + (size_t)sr * W * 3,
+                    const size_t dr = (size_t)dstRow(e);
+                    if (out_rgb) std::memcpy(out_rgb + dr * W * 3, r.host_rgb + (size_t)sr * W * 3,
                                              (size_t)nr * W * 3 * sizeof(double));
-                    if (out_rgba8) std::memcpy(out_rgba8 + (size_t)rowOff[e] * W * 4, r.host_rgba + (size_t)sr * W * 4,
+                    if (out_rgba8) std::memcpy(out_rgba8 + dr * W * 4, r.host_rgba + (size_t)sr * W * 4,
                                                (size_t)nr * W * 4);
                 }
             };
@@ -1036,7 +1093,7 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
         HIP_TRY(hipEventRecord(s->devs[k].ev1, s->devs[k].stream));
     }
     double km = 0;
-    int64_t sh = 0, se = 0;
+    int64_t sh = 0, se = 0, st = 0;
     for (int32_t k = 0; k < D; ++k) {
         if (plan[k].nb == 0) continue;
         DeviceReplica& r = s->devs[k];
@@ -1044,7 +1101,7 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
         HIP_TRY(hipStreamSynchronize(r.stream));
         unsigned long long c[kCounterWords];
         HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
-        sh += (int64_t)c[0]; se += (int64_t)c[1];
+        sh += (int64_t)c[0]; se += (int64_t)c[1]; st += (int64_t)c[kCounterShadowTraced];
         float ms = 0; (void)hipEventElapsedTime(&ms, r.ev0, r.ev1);
         km = std::max(km, (double)ms);
     }
@@ -1055,7 +1112,33 @@ int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double*
         const int64_t n = (int64_t)std::sqrt((double)std::max(1, C.num_samples));
         stats->primary_rays = (int64_t)rowsTotal * W * n * n;
         stats->shadow_rays = sh; stats->secondary_rays = se; stats->kernel_ms = km;
+        stats->shadow_rays_traced = st;
         stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return RT_OK;
+}
+
+int32_t rt_render(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb, uint8_t* out_rgba8,
+                  rt_stats* stats, rt_progress_fn progress, void* user) {
+    return rt_render_ex(s, cam, first, step, out_rgb, out_rgba8, 0u, stats, progress, user);
+}
+
+int32_t rt_host_register(void* ptr, uint64_t bytes) {
+    if (!ptr || bytes == 0) return fail(RT_ERR_INVALID_ARG, "null or empty host range");
+    const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(RT_ERR_DEVICE, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    }
+    return RT_OK;
+}
+
+int32_t rt_host_unregister(void* ptr) {
+    if (!ptr) return RT_OK;
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(RT_ERR_DEVICE, std::string("hipHostUnregister: ") + hipGetErrorString(e));
     }
     return RT_OK;
 }
@@ -1132,6 +1215,11 @@ static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o,
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     RenderParams P = make_params(s, r, 0, 0, 1, nullptr, nullptr);
+    {   // margin for these rays' own origins
+        double od = 0.0;
+        for (int32_t k = 0; k < n; ++k) od = std::max(od, dist_to_center(s->host, o + 3 * (size_t)k));
+        P.prune_abs = prune_abs_for(s->host, od);
+    }
     dev::RayBatch B{};
     B.n = n;
     const char* ue = std::getenv("MYRT_UNIFIED");

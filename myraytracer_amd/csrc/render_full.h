@@ -92,6 +92,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                             c.shadow++;
                             const double NdotL = smax(0.0, dot(N, wi));
                             if (NdotL > 0 || MYRT_REF(P)) {                 // else the result is discarded
+                                c.shadow_traced++;
                                 const bool blocked = occluded<COUNT>(P, p + wi * P.shadow_eps, wi, dist, time, st, c);
                                 if (!blocked && NdotL > 0) {
                                     const double shininess = smax(1.0, M.phong);
@@ -128,6 +129,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                         const double Ln = fabs(dot(nL, -wi));
                         if (Ln <= 0) continue;
                         c.shadow++;
+                        c.shadow_traced++;
                         if (occluded<COUNT>(P, p + wi * P.shadow_eps, wi, dist - P.shadow_eps, time, st, c)) continue;
                         const V3 view = normalize(-d);
                         const V3 hv = normalize(wi + view);
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(256) void k_events(RenderParams P) {
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
     if (i >= P.cam.width || j >= P.cam.height) return;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{};
     MYRT_STACK(st, lds_stack);
     long long events = 0;
     (void)pixel_full<false, true>(P, i, j, events, st, cnt);
@@ -340,12 +342,13 @@ __global__ __launch_bounds__(256) void render_full(RenderParams P) {
     full_pixel_of(P, i, j, slot, row);
     const bool valid = (i < P.cam.width) && (j < P.cam.height);
     const int lane = threadIdx.x & 63;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{};
     if (valid) {
         MYRT_STACK(st, lds_stack);
-        const size_t o = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
-        long long jitterIndex = P.num_alights > 0 ? P.jstart[o] : 0;
+        const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;   // packed selection index
+        long long jitterIndex = P.num_alights > 0 ? P.jstart[q] : 0;
         const V3 px = pixel_full<COUNT, false>(P, i, j, jitterIndex, st, cnt) / (double)P.cam.samples;
+        const size_t o = out_row_of(P, j >> 3, row) * (size_t)P.cam.width + i;
         if (P.out_rgb) {
             P.out_rgb[o * 3 + 0] = px.x;
             P.out_rgb[o * 3 + 1] = px.y;
@@ -359,10 +362,12 @@ __global__ __launch_bounds__(256) void render_full(RenderParams P) {
             reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
         }
     }
-    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary);
+    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
+                             s2 = wave_sum(cnt.shadow_traced);
     if (lane == 0) {
         if (s0) atomicAdd(&P.counters[0], s0);
         if (s1) atomicAdd(&P.counters[1], s1);
+        if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
     }
     if (COUNT) {
         const unsigned long long a = wave_sum(cnt.recs), b = wave_sum(cnt.tris), cc = wave_sum(cnt.normals),

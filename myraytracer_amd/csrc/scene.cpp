@@ -598,6 +598,10 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             P = o.positions; nPos = o.num_positions; I = o.indices; nIdx = o.num_indices;
             Nn = o.normals; off = o.indices_one_based ? 1 : 0;
             if ((nPos > 0 && !P) || (nIdx > 0 && !I)) { err = "mesh arrays missing"; return RT_ERR_INVALID_ARG; }
+            if (Nn && o.num_normals != nPos) {
+                err = "mesh normals: num_normals must equal num_positions";
+                return RT_ERR_INVALID_ARG;
+            }
         }
         phase("ply");
         const bool isSmooth = o.smooth != 0;
@@ -701,7 +705,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
 
     phase("flatten");
     // ---- BLAS builds (buildBLASForMesh: maxLeaf 2, SAH, 12 bins; RTContext.swift:430-435)
-    int64_t maxBlasDepth = 0;
+    int64_t maxBlasDepth = 0, tlasDepth = 0;
     for (auto& bb : blases) {
         bb.bvh = build_ref_bvh(bb.prims, 2, 12);
         bb.hash = ref_bvh_hash(bb.bvh, bb.triIndex);
@@ -790,6 +794,39 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
     }
 
     phase("layout");
+    // ---- pruning margin (DESIGN.md "Pruning"): a culled node may only hold triangles whose
+    // Moeller-Trumbore t, as computed, can not undercut the current hit.  MT's t = num/det
+    // with |det| >= eps carries an absolute error below
+    //   8u * |e1||e2| * (|o - v0| + t|d|) / eps      (u = 2^-53; both triple products),
+    // in the instance's local frame, where |d| and |o - v0| are at most ||A||_F times their
+    // world values (A = the linear part of worldToLocal).  Planes: 8u |n| (...) / eps.  The
+    // scene constant prune_k = 8u/eps * max over instances of P_blas * ||A||_F is turned into
+    // an absolute margin per render from the ray origins' distance to the scene (make_params).
+    std::vector<double> blasP(blases.size(), 0.0);
+    {
+        const int TP = std::max(1, std::min<int>(build_threads(), (int)(triangles.size() / 262144)));
+        for (size_t b = 0; b < blases.size(); ++b) {
+            const BlasBuild& bb = blases[b];
+            if (bb.kind == kPrimPlane) {
+                const TriRec& t = S.tris[bb.tri_first];
+                blasP[b] = std::sqrt(t.e1[0] * t.e1[0] + t.e1[1] * t.e1[1] + t.e1[2] * t.e1[2]);
+                continue;
+            }
+            if (bb.kind != kPrimTriangles) continue;          // spheres: covered by prune_rel
+            std::vector<double> part(TP, 0.0);
+            const int64_t n = (int64_t)bb.triIndex.size();
+            run_chunks(TP, [&](int kc) {
+                double m = 0.0;
+                for (int64_t q = n * kc / TP, qe = n * (kc + 1) / TP; q < qe; ++q) {
+                    const Tri& t = triangles[bb.triIndex[q]];
+                    m = std::fmax(m, std::sqrt(dot(t.e1, t.e1)) * std::sqrt(dot(t.e2, t.e2)));
+                }
+                part[kc] = m;
+            });
+            for (double m : part) blasP[b] = std::fmax(blasP[b], m);
+        }
+    }
+    double pruneK = 0.0, maxMotion = 0.0;
     // ---- instances (makeInstance, RTContext.swift:437-457) and TLAS (buildTLAS :459-474)
     PrimSet tp;
     tp.n = (int64_t)insts.size();
@@ -829,6 +866,13 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         DInstance di{};
         std::memcpy(di.l2w, ib.M, sizeof(di.l2w));
         m4_inverse(ib.M, di.w2l);
+        {
+            double fro = 0.0;
+            for (int c = 0; c < 3; ++c)
+                for (int r = 0; r < 3; ++r) fro += di.w2l[c * 4 + r] * di.w2l[c * 4 + r];
+            pruneK = std::fmax(pruneK, blasP[ib.blas] * std::sqrt(fro));
+            maxMotion = std::fmax(maxMotion, std::sqrt(dot(ib.motion, ib.motion)) + std::sqrt(dot(bb.motion, bb.motion)));
+        }
         normal_matrix(ib.M, di.nmat);
         di.motion[0] = ib.motion.x; di.motion[1] = ib.motion.y; di.motion[2] = ib.motion.z;
         di.tri_motion[0] = bb.motion.x; di.tri_motion[1] = bb.motion.y; di.tri_motion[2] = bb.motion.z;
@@ -859,10 +903,23 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         S.tlas_root_ref = layout_bvh(tb, S.recs, emit);
         S.tlas_records = (int64_t)S.recs.size() - S.blas_records;
         S.has_tlas = true;
-        S.max_stack = (tdepth + 1) + (maxBlasDepth + 1) + 2;
+        // Stack entries a walk can hold (device.h Stack, kStackCap): one deferred far child per
+        // inner node on the current path, TLAS path below BLAS path (+2 slack).  The unified
+        // identity walk also pushes a whole TLAS leaf's instance roots at once.
+        int64_t maxTlasLeaf = 1;
+        for (int64_t n = 0; n < tb.nodesUsed; ++n)
+            if (tb.isLeaf(n)) maxTlasLeaf = std::max(maxTlasLeaf, tb.count[n]);
+        S.max_stack = tdepth + maxBlasDepth + 2;
+        S.max_stack_unified = tdepth + maxTlasLeaf + maxBlasDepth + 2;
+        tlasDepth = tdepth;
         const double dx = whi[0] - wlo[0], dy = whi[1] - wlo[1], dz = whi[2] - wlo[2];
         S.scene_extent = std::sqrt(dx * dx + dy * dy + dz * dz);
         if (!std::isfinite(S.scene_extent) || S.scene_extent <= 0) S.scene_extent = 1.0;
+        for (int k = 0; k < 3; ++k) S.scene_center[k] = 0.5 * (wlo[k] + whi[k]);
+        if (!std::isfinite(S.scene_center[0] + S.scene_center[1] + S.scene_center[2]))
+            S.scene_center[0] = S.scene_center[1] = S.scene_center[2] = 0.0;
+        S.prune_k = (S.eps > 0) ? 8.0 * std::ldexp(1.0, -53) * pruneK / S.eps : kInf;
+        S.max_motion = maxMotion;
     }
     // Identity mode: every instance's transforms are exactly the identity and nothing moves,
     // so the world ray IS the local ray (up to the sign of zeros, which no comparison sees)
@@ -881,6 +938,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         }
         for (int o : owners) ident &= (o <= 1);
         ident &= !S.has_special;                    // the unified walk tests triangles only
+        ident &= S.max_stack_unified <= kStackCap;  // else the general walk (fewer entries)
         S.identity = ident;
         if (ident) {
             for (size_t i = 0; i < insts.size(); ++i) {
@@ -893,7 +951,14 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         }
     }
     if (S.recs.size() >= (size_t)INT32_MAX || S.tris.size() >= (size_t)INT32_MAX) { err = "scene too large for int32 refs"; return RT_ERR_UNSUPPORTED; }
-    if (maxBlasDepth + 1 > 63) { err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550)"; return RT_ERR_STACK; }
+    if (maxBlasDepth + 1 > 63 || tlasDepth + 1 > 63) {
+        err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550, 623)";
+        return RT_ERR_STACK;
+    }
+    if (S.max_stack > kStackCap) {                  // unreachable while kStackCap >= 2*63+2
+        err = "BVH deeper than the device traversal stack";
+        return RT_ERR_STACK;
+    }
     phase("tlas+inst");
     S.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;

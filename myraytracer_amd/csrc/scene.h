@@ -67,8 +67,12 @@ struct HostScene {
     bool has_tlas = false;
     bool identity = false;                 // all instances identity & static (unified walk)
     int64_t blas_records = 0, tlas_records = 0;
-    int64_t max_stack = 0;                 // LDS stack entries a traversal needs
+    int64_t max_stack = 0;                 // traversal stack entries the general walk needs
+    int64_t max_stack_unified = 0;         // ... and the unified identity walk
     double scene_extent = 1.0;             // world bounds diagonal (pruning margin scale)
+    double scene_center[3] = {0, 0, 0};    // world bounds center
+    double prune_k = 0.0;                  // MT t-error constant (scene.cpp, "pruning margin")
+    double max_motion = 0.0;               // largest instance + triangle motion-blur offset
     // ---- bookkeeping / debug
     int64_t n_meshes = 0, n_tris = 0, n_spheres = 0, n_planes = 0;
     std::vector<uint64_t> inst_bvh_hash;   // per instance: canonical hash of its BLAS

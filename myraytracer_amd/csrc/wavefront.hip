@@ -69,8 +69,9 @@ __device__ __forceinline__ PixelOf pixel_of(const WaveParams& W, int64_t slot) {
     PixelOf p;
     p.i = tileX * 8 + (lane & 7);
     const int r = lane >> 3;
-    p.j = (W.R.chunk_first + chunkSlot * W.R.chunk_step) * 8 + r;
-    p.outRow = chunkSlot * 8 + r;
+    const int chunk = W.R.chunk_first + chunkSlot * W.R.chunk_step;
+    p.j = chunk * 8 + r;
+    p.outRow = (int)out_row_of(W.R, chunk, r);
     p.valid = p.i < W.R.cam.width && p.j < W.R.cam.height;
     return p;
 }
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(256) void k_persist(WaveParams W, int64_t N, unsign
     const RenderParams& P = W.R;
     constexpr bool SHADOW = (MODE == 2);
     MYRT_STACK(st, lds_stack);
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{};
     const int lane = lane_id();
     const unsigned long long ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     WaveWork w{0, 0, (int)(blockIdx.x & 7), 0, false};
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(256) void k_persist(WaveParams W, int64_t N, unsign
     // ray counters: shadow rays (MODE 2) and secondary rays (MODE 1), one atomic per wave
     const unsigned long long nr = wave_sum((unsigned long long)rays);
     if (lane == 0 && nr) {
-        if (MODE == 2) atomicAdd(&P.counters[0], nr);
+        if (MODE == 2) { atomicAdd(&P.counters[0], nr); atomicAdd(&P.counters[kCounterShadowTraced], nr); }
         if (MODE == 1) atomicAdd(&P.counters[1], nr);
     }
     flush_counts(W, cnt, COUNT);
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(256) void k_general(WaveParams W, int64_t N) {
     extern __shared__ unsigned long long lds_stack[];
     const RenderParams& P = W.R;
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{};
     unsigned rays = 0;
     V3 o, d;
     double tlo, tmax, time;
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(256) void k_general(WaveParams W, int64_t N) {
     }
     const unsigned long long nr = wave_sum((unsigned long long)rays);
     if (lane_id() == 0 && nr) {
-        if (MODE == 2) atomicAdd(&P.counters[0], nr);
+        if (MODE == 2) { atomicAdd(&P.counters[0], nr); atomicAdd(&P.counters[kCounterShadowTraced], nr); }
         if (MODE == 1) atomicAdd(&P.counters[1], nr);
     }
     flush_counts(W, cnt, COUNT);
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(256) void k_shade(WaveParams W) {
     const int depth = W.depth;
     const int64_t path = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (path >= W.P) return;
-    Counts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counts cnt{};
     const int L = P.num_plights;
     bool active;
     TraceItem it;

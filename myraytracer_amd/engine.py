@@ -69,6 +69,11 @@ class RenderStats:                       # Models/RenderStats.swift:8-24 (+ ray 
     secondary_rays: int
     milliseconds: float
     kernel_ms: float
+    shadow_rays_traced: int = 0          # shadow rays whose any-hit walk ran (<= shadow_rays)
+
+    @property
+    def rays_traced(self) -> int:
+        return self.primary_rays + self.shadow_rays_traced
 
 
 @dataclass
@@ -201,6 +206,26 @@ class RayTracerEngine:
             rgba = out_rgba
         else:
             rgba = np.empty((rows, W, 4), dtype=np.uint8)
+        stats = self.render_into(camera_index, chunk_first, chunk_step, rgb, rgba, progress=progress)
+        return rgb, rgba, stats
+
+    def render_into(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
+                    rgb: Optional[np.ndarray] = None, rgba: Optional[np.ndarray] = None,
+                    frame_layout: bool = False,
+                    progress: Optional[Callable[[RenderProgress], bool]] = None) -> RenderStats:
+        """rt_render_ex into caller-owned arrays (either may be None).  Shapes: the selected
+        rows packed, (rows, W, 3|4); with frame_layout the whole frame (H, W, 3|4), the
+        selected chunks' rows written at their image rows (RT_RENDER_FRAME_LAYOUT)."""
+        lib = load_library()
+        if not (0 <= camera_index < len(self.scene.cameras)):
+            raise RenderError(A.RT_ERR_INVALID_CAMERA, "Invalid camera index")
+        cam = self.scene.cameras[camera_index]
+        W, H = max(1, int(cam.image_resolution[0])), max(1, int(cam.image_resolution[1]))
+        rows = H if frame_layout else lib.rt_rows_for_chunks(H, chunk_first, chunk_step)
+        for a, ch, dt in ((rgb, 3, np.float64), (rgba, 4, np.uint8)):
+            if a is not None and (a.shape != (rows, W, ch) or a.dtype != dt or not a.flags.c_contiguous):
+                raise ValueError(f"output array must be C-contiguous {dt.__name__}{(rows, W, ch)}, got "
+                                 f"{a.dtype}{a.shape}")
         st = A.rt_stats()
 
         def _cb(user, done, total):
@@ -209,14 +234,11 @@ class RayTracerEngine:
             return 1 if progress(RenderProgress(done / max(total, 1), f"Row {done}/{total}")) else 0
 
         cb = A.RT_PROGRESS_FN(_cb) if progress is not None else A.RT_PROGRESS_FN()
-        _check(lib.rt_render(self._h, camera_index, chunk_first, chunk_step,
-                             rgb.ctypes.data_as(A.c_double_p),
-                             rgba.ctypes.data_as(C.POINTER(C.c_uint8)) if rgba is not None else None,
-                             C.byref(st), cb, None))
-        stats = RenderStats(int(st.meshes), int(st.triangles), int(st.spheres), int(st.planes),
-                            int(st.primary_rays + st.shadow_rays), int(st.primary_rays), int(st.shadow_rays),
-                            int(st.secondary_rays), float(st.milliseconds), float(st.kernel_ms))
-        return rgb, rgba, stats
+        _check(lib.rt_render_ex(self._h, camera_index, chunk_first, chunk_step,
+                                rgb.ctypes.data_as(A.c_double_p) if rgb is not None else None,
+                                rgba.ctypes.data_as(C.POINTER(C.c_uint8)) if rgba is not None else None,
+                                A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0, C.byref(st), cb, None))
+        return _stats(st)
 
     def render(self, camera_index: int = 0, progress: Optional[Callable[[RenderProgress], bool]] = None) -> RenderResult:
         """RayTracerEngine.render(format:cameraIndex:progress:) (RayTracer.swift:115-131)."""
@@ -279,6 +301,23 @@ class RayTracerEngine:
 
     def bvh_hash(self, instance: int) -> int:
         return int(load_library().rt_debug_bvh_hash(self._h, instance))
+
+
+def _stats(st: A.rt_stats) -> RenderStats:
+    return RenderStats(int(st.meshes), int(st.triangles), int(st.spheres), int(st.planes),
+                       int(st.primary_rays + st.shadow_rays), int(st.primary_rays), int(st.shadow_rays),
+                       int(st.secondary_rays), float(st.milliseconds), float(st.kernel_ms),
+                       int(st.shadow_rays_traced))
+
+
+def register_host(arr: np.ndarray):
+    """Page-lock an existing host array (rt_host_register; e.g. a framebuffer in shared memory
+    that several processes fill).  Call unregister_host(arr) before the memory goes away."""
+    _check(load_library().rt_host_register(C.c_void_p(arr.ctypes.data), arr.nbytes))
+
+
+def unregister_host(arr: np.ndarray):
+    _check(load_library().rt_host_unregister(C.c_void_p(arr.ctypes.data)))
 
 
 def _ray_arrays(origins, dirs, tlim, time):

@@ -213,8 +213,12 @@ class PackedScene:
                     r.indices_one_based = 1 if o.indices_one_based else 0
                     if o.normals is not None:
                         nrm = np.ascontiguousarray(o.normals, dtype=np.float64).reshape(-1)
+                        if nrm.size != pos.size:
+                            raise ValueError(f"mesh normals: {nrm.size // 3} xyz triples for "
+                                             f"{pos.size // 3} positions (one normal per vertex expected)")
                         self._keep.append(nrm)
                         r.normals = nrm.ctypes.data_as(A.c_double_p)
+                        r.num_normals = nrm.size // 3
             elif isinstance(o, Triangle):
                 r.kind = A.RT_OBJ_TRIANGLE
                 r.material_id = material_index(o.material)

@@ -27,7 +27,7 @@ class oracle_stats(C.Structure):
     _fields_ = [("primary_rays", C.c_int64), ("shadow_rays", C.c_int64), ("secondary_rays", C.c_int64),
                 ("node_visits", C.c_int64), ("node_fetches", C.c_int64), ("tri_tests", C.c_int64),
                 ("smooth_hits", C.c_int64), ("pixels", C.c_int64), ("milliseconds", C.c_double),
-                ("threads", C.c_int32)]
+                ("threads", C.c_int32), ("shadow_rays_used", C.c_int64)]
 
 
 _lib = None

@@ -329,9 +329,11 @@ struct Ray {                                                          // Parsing
 struct Counters {
     int64_t primary = 0, shadow = 0, secondary = 0, visits = 0;
     int64_t nodeFetch = 0, triTest = 0, smoothHit = 0, pixels = 0;
+    int64_t shadowUsed = 0;   // shadow rays whose result trace() uses (point lights: N.L > 0)
     void add(const Counters& o) {
         primary += o.primary; shadow += o.shadow; secondary += o.secondary; visits += o.visits;
         nodeFetch += o.nodeFetch; triTest += o.triTest; smoothHit += o.smoothHit; pixels += o.pixels;
+        shadowUsed += o.shadowUsed;
     }
 };
 
@@ -955,6 +957,7 @@ struct Renderer {
                 Ray sRay(p + wi * shadowEps, wi, inRay.time);
                 sRay.tMax = dist;
                 k.shadow += 1;
+                if (smax(0.0, dot(N, wi)) > 0) k.shadowUsed += 1;   // (instrumentation only)
                 bool blocked = occluded(sRay, k);
                 if (!blocked) {
                     double NdotL = smax(0.0, dot(N, wi));
@@ -992,6 +995,7 @@ struct Renderer {
                 Ray sRay(p + wi * shadowEps, wi, inRay.time);
                 sRay.tMax = dist - shadowEps;
                 k.shadow += 1;
+                k.shadowUsed += 1;
                 if (occluded(sRay, k)) continue;
                 V3 view = normalize(-inRay.dir);
                 V3 h = normalize(wi + view);
@@ -1150,6 +1154,7 @@ typedef struct oracle_stats {
     int64_t node_fetches, tri_tests, smooth_hits, pixels;
     double milliseconds;
     int32_t threads;
+    int64_t shadow_rays_used;   /* shadow rays whose result is used (the GPU's shadow_rays_traced) */
 } oracle_stats;
 
 const char* oracle_last_error(void) { return orc::g_err.c_str(); }
@@ -1235,6 +1240,7 @@ int32_t oracle_render(void* scene, int32_t camera_index, int32_t chunk_first, in
         stats->smooth_hits = tot.smoothHit; stats->pixels = tot.pixels;
         stats->milliseconds = std::chrono::duration<double, std::milli>(t1 - t0).count();
         stats->threads = nthreads;
+        stats->shadow_rays_used = tot.shadowUsed;
     }
     return RT_OK;
 }

@@ -1,0 +1,170 @@
+"""Full-frame GPU parity on exactly what bench.py times, and the multi-GPU gather.
+
+* C3 (1.02M tris, 1920x1080) loaded from its PLY with default settings, rendered through
+  rt_render_ex into page-locked whole-frame buffers (the bench's headline path: the kernels
+  store the rows into host memory) and through rt_render_device (the device-only side path),
+  each compared on the FULL frame with the oracle ("check all of C1-C3").
+* C2 at its full 800x600.
+* C4: the C3 frame rendered by 8 replicas (chunk c on replica c mod 8), equal to the oracle and
+  to the 1-replica frame; disjoint chunk selections gathered into one frame (frame layout).
+* bench.py --gpus 2 (two ranks on this one GPU): the strong split gathers a complete frame
+  bit-identical to the 1-GPU frame.
+Bar: per-channel L-inf <= 1e-5 on FP64, exact RGBA8, equal ray counts.
+"""
+import copy
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import myraytracer_amd as M
+from myraytracer_amd import scenes
+import oracle
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _inline(scene):
+    """The PLY-loaded scene as inline arrays read by the product's PLY reader (the oracle takes
+    arrays; the reader itself is pinned against the reference's CPly, tests/test_ply.py)."""
+    s = copy.deepcopy(scene)
+    for obj in s.objects:
+        if isinstance(obj, M.Mesh) and obj.ply_path is not None:
+            m = M.ply_load(obj.ply_path)
+            obj.positions, obj.indices, obj.normals = m["positions"], m["indices"], m["normals"]
+            obj.indices_one_based = False
+            obj.ply_path = None
+    return s
+
+
+@pytest.fixture(scope="module")
+def c3_ply(scene_dir):
+    sc = scenes.scene_c3(path_dir=scene_dir)
+    ref, ref8, ost = oracle.OracleScene(_inline(sc)).render(0, threads=0, rgba=True)
+    return sc, ref, ref8, ost
+
+
+def _assert_frame(rgb, rgba, ref, ref8):
+    if rgb is not None:
+        d = np.abs(rgb - ref)
+        assert float(d.max()) <= TOL, f"L-inf {float(d.max()):.3e} on {int((d > TOL).any(-1).sum())} px"
+    if rgba is not None:
+        assert np.array_equal(rgba, ref8), f"RGBA8 differs on {int((rgba != ref8).any(-1).sum())} px"
+
+
+def test_c3_full_frame_bench_path(c3_ply, monkeypatch):
+    monkeypatch.delenv("MYRT_PATH", raising=False)
+    sc, ref, ref8, ost = c3_ply
+    eng = M.RayTracerEngine(sc)
+    H, W = ref.shape[:2]
+    rgba = M.pinned_array((H, W, 4), np.uint8)
+    rgb = M.pinned_array((H, W, 3), np.float64)
+    rgba.fill(0)
+    st = eng.render_into(0, 0, 1, rgb=None, rgba=rgba, frame_layout=True)     # bench.py's headline call
+    _assert_frame(None, rgba, ref, ref8)
+    assert st.primary_rays == ost.primary_rays and st.shadow_rays == ost.shadow_rays
+    assert st.shadow_rays_traced == ost.shadow_rays_used
+    st2 = eng.render_into(0, 0, 1, rgb=rgb, rgba=None, frame_layout=True)     # fp64 side path
+    _assert_frame(rgb, None, ref, ref8)
+    assert st2.shadow_rays_traced == st.shadow_rays_traced
+    eng.close()
+
+
+def test_c3_full_frame_device_path(c3_ply, monkeypatch):
+    import torch
+    monkeypatch.delenv("MYRT_PATH", raising=False)
+    sc, ref, ref8, _ = c3_ply
+    eng = M.RayTracerEngine(sc)
+    H, W = ref.shape[:2]
+    out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    out8 = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    eng.render_device(out.data_ptr(), 0, 0, 1, stream=s.cuda_stream, out_rgba_ptr=out8.data_ptr())
+    s.synchronize()
+    _assert_frame(out.cpu().numpy(), out8.cpu().numpy(), ref, ref8)
+    eng.close()
+
+
+def test_c4_eight_replicas_full_c3(c3_ply, monkeypatch):
+    """configs[3]: the C3 frame split over 8 replicas (8-row chunk c on replica c mod 8; here all
+    on the one GPU of the box), gathered by rt_render into one page-locked frame."""
+    monkeypatch.delenv("MYRT_PATH", raising=False)
+    sc, ref, ref8, ost = c3_ply
+    H, W = ref.shape[:2]
+    eng8 = M.RayTracerEngine(sc, devices=[0] * 8)
+    rgb = M.pinned_array((H, W, 3), np.float64)
+    rgba = M.pinned_array((H, W, 4), np.uint8)
+    rgb.fill(-1.0)
+    rgba.fill(0)
+    st = eng8.render_into(0, 0, 1, rgb=rgb, rgba=rgba)
+    _assert_frame(rgb, rgba, ref, ref8)
+    assert st.shadow_rays == ost.shadow_rays and st.shadow_rays_traced == ost.shadow_rays_used
+    # the staged path (pageable buffers) gathers the same image
+    r2, r28, _ = eng8.render_rows(0, 0, 1, True)
+    assert np.array_equal(r2, rgb) and np.array_equal(r28, rgba)
+    eng8.close()
+
+
+def test_c2_full_frame():
+    sc = scenes.scene_c2(inline=True)            # 800x600, every chunk
+    eng = M.RayTracerEngine(sc)
+    rgb, rgba, st = eng.render_rows(0, 0, 1, True)
+    ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
+    _assert_frame(rgb, rgba, ref, ref8)
+    assert (st.primary_rays, st.shadow_rays) == (ost.primary_rays, ost.shadow_rays)
+    eng.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_frame_layout_gathers_disjoint_selections(devices):
+    """RT_RENDER_FRAME_LAYOUT: selections k, k+3, ... (k = 0, 1, 2) fill one whole frame; rows
+    outside a selection are left untouched."""
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 136, 100)     # 13 chunks, last partial
+    eng = M.RayTracerEngine(sc, devices=devices)
+    full, full8, _ = eng.render_rows(0, 0, 1, True)
+    for pinned in (True, False):
+        if pinned:
+            rgb, rgba = M.pinned_array((100, 136, 3), np.float64), M.pinned_array((100, 136, 4), np.uint8)
+        else:
+            rgb, rgba = np.empty((100, 136, 3)), np.empty((100, 136, 4), np.uint8)
+        rgb.fill(-7.0)
+        rgba.fill(3)
+        eng.render_into(0, 1, 3, rgb=rgb, rgba=rgba, frame_layout=True)
+        sel = np.zeros(100, bool)
+        for c in range(1, 13, 3):
+            sel[8 * c: 8 * c + 8] = True
+        assert np.array_equal(rgb[sel], full[sel]) and np.array_equal(rgba[sel], full8[sel])
+        assert np.all(rgb[~sel] == -7.0) and np.all(rgba[~sel] == 3)
+        for k in (0, 2):
+            eng.render_into(0, k, 3, rgb=rgb, rgba=rgba, frame_layout=True)
+        assert np.array_equal(rgb, full) and np.array_equal(rgba, full8)
+    eng.close()
+
+
+def _bench(args, env_extra):
+    env = dict(os.environ, **env_extra)
+    env.pop("MYRT_PATH", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_strong_split_two_ranks_gathers_the_same_frame():
+    """`bench.py --gpus 2` (torchrun started by bench.py, both ranks pinned to this GPU): one C2
+    frame per step, chunks split over the ranks, rows stored into one shared page-locked
+    framebuffer - complete and bit-identical to the 1-GPU frame."""
+    common = ["--config", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-side-paths"]
+    one = _bench(["--gpus", "1"] + common, {})
+    two = _bench(["--gpus", "2"] + common, {"MYRT_BENCH_DEVICE": "0"})
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["scaling"] == "strong"
+    assert one["gather"]["rows_complete"] and two["gather"]["rows_complete"]
+    assert two["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
+    assert two["rays"]["per_step"] == one["rays"]["per_step"]

@@ -4,6 +4,7 @@ Bar (BASELINE.json north_star): per-channel L-inf <= 1e-5 on the FP64 framebuffe
 plus exact RGBA8 equality.  Every test renders through libmyrt.so on cuda:0.
 """
 import copy
+import os
 
 import numpy as np
 import pytest
@@ -37,6 +38,11 @@ def _compare(sc, chunk_first=0, chunk_step=1, cam=0, tol=TOL, check_rgba=True):
     assert st.primary_rays == ost.primary_rays
     assert st.shadow_rays == ost.shadow_rays, (st.shadow_rays, ost.shadow_rays)
     assert st.secondary_rays == ost.secondary_rays, (st.secondary_rays, ost.secondary_rays)
+    # shadow walks actually run: the megakernels skip the ones whose result the reference
+    # discards (N.L <= 0); the wavefront pipeline traces every cast ray
+    assert ost.shadow_rays_used <= st.shadow_rays_traced <= st.shadow_rays
+    if os.environ.get("MYRT_PATH") != "wave":
+        assert st.shadow_rays_traced == ost.shadow_rays_used, (st.shadow_rays_traced, ost.shadow_rays_used)
     eng.close()
     return linf, st
 

@@ -128,3 +128,56 @@ def test_motion_blur_times_and_tmin():
     O, D = _ray_set(np.array([0.0, 0.0, 0.0]), 2.5, 2000, 9)
     rng = np.random.RandomState(2)
     _check_closest(sc, O, D, tmin=rng.uniform(0.0, 0.5, size=len(O)), time=rng.uniform(0, 1, size=len(O)))
+
+
+def _rotation(rng):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+@pytest.mark.parametrize("walk", ["unified", "general"])
+def test_near_degenerate_grazing_hits_and_the_pruning_margin(walk, monkeypatch):
+    """Large, nearly coplanar triangles and rays grazing them through a corner (|det| just
+    above eps): Moeller-Trumbore's t then carries an error of up to ~1e-4 relative and can
+    undercut the entry distance of the triangle's own box - far beyond the round-1 margin
+    (1e-7 rel + 1e-9 diag), measured on CPU.  The margin now bounds that error
+    (scene.cpp, "pruning margin"), so pruning still never drops a node whose triangle the
+    reference would accept: hits stay bit-identical to the unpruned oracle."""
+    monkeypatch.setenv("MYRT_UNIFIED", "1" if walk == "unified" else "0")
+    rng = np.random.default_rng(17)
+    R0 = _rotation(rng)
+    V, F, corners = [], [], []
+    for k in range(48):
+        L = 10 ** rng.uniform(1.7, 2.7)
+        Rk = R0 @ _rotation(np.random.default_rng(1000 + k))[:, :] if k % 4 == 0 else R0
+        tilt = np.eye(3) + rng.normal(scale=1e-9, size=(3, 3))
+        v0 = rng.normal(scale=1e-6, size=3) + np.array([0.0, 0.0, 0.05 * (k % 3)])
+        e1 = Rk @ tilt @ np.array([L, 0.0, 0.0])
+        e2 = Rk @ tilt @ np.array([0.3 * L, L, 0.0])
+        V += [v0, v0 + e1, v0 + e2]
+        F.append([3 * k, 3 * k + 1, 3 * k + 2])
+        corners.append((v0, e1, e2, Rk @ np.array([0.0, 0.0, 1.0])))
+    mesh = M.Mesh(id=1, material="1", positions=np.array(V), indices=np.array(F, np.int32),
+                  indices_one_based=False, shading_mode="flat")
+    sc = scenes.scaled(scenes.scene_c1(8, 8), 8, 8)
+    sc.objects = [mesh]
+    O, D = [], []
+    for i in range(6000):
+        v0, e1, e2, nrm = corners[rng.integers(len(corners))]
+        tgt = v0 + rng.uniform(0, 1e-9) * e1 + rng.uniform(0, 1e-9) * e2
+        inplane = (e1 + e2) / np.linalg.norm(e1 + e2) + rng.uniform(-0.1, 0.1) * e1 / np.linalg.norm(e1)
+        inplane /= np.linalg.norm(inplane)
+        d = inplane + 10 ** rng.uniform(-13, -7) * rng.choice([-1.0, 1.0]) * nrm
+        d /= np.linalg.norm(d)
+        O.append(tgt - d * 10 ** rng.uniform(0, 3))
+        D.append(d)
+    O, D = np.array(O), np.array(D)
+    hit = _check_closest(sc, O, D)
+    assert hit.mean() > 0.3
+    t, *_ = oracle.OracleScene(sc).trace_rays(O, D)
+    tmax = np.where(np.isfinite(t), t * (1 + rng.choice([-1e-12, 1e-12], size=len(t))), 1e3)
+    _check_occluded(sc, O, D, tmax)

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Roofline summary of the render megakernel from rocprofv3 passes (one counter group per pass).
+
+usage: pmc_roofline.py --kernel 'render_kernel<false, false, true>' --trace DIR --fetch DIR --write DIR
+                       --td DIR [--sq DIR] --lib myraytracer_amd/libmyrt.so -o profiles/roofline_c3.json
+
+Per launch (median over the dispatches of that kernel):
+  hbm_bytes_per_launch = FETCH_SIZE x 2 + WRITE_SIZE (KB -> B).  /opt/skills/guides/MI355X_MICROARCH.md,
+      "HBM": on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so it reads half the bytes; both
+      counters include Infinity-Cache (MALL) hits, so this is an upper bound on DRAM bytes.
+  td_busy  = (TD_TD_BUSY_sum / 256 CUs) / (GRBM_GUI_ACTIVE / 8 XCDs): texture-data (vector-memory
+      return) path utilisation - the resource that binds this kernel.
+  ta_busy  = TA_BUSY_avr / (GRBM_GUI_ACTIVE / 8).
+  valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)  (needs --sq).
+  kernel_ms = average duration from the --kernel-trace --stats pass.
+lib_sha256_16 ties the summary to the library build it measured (bench.py checks it).
+"""
+import argparse
+import csv
+import glob
+import hashlib
+import json
+import os
+import statistics
+
+
+def _files(path, pattern):
+    if os.path.isfile(path):
+        return [path]
+    return glob.glob(os.path.join(path, "**", pattern), recursive=True)
+
+
+def counter(path, name, kernel):
+    vals = {}
+    for f in _files(path, "*counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != name or kernel not in r["Kernel_Name"]:
+                continue
+            key = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(vals))
+            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no {name} rows for kernel {kernel!r} under {path}")
+    return statistics.median(vals.values()), len(vals)
+
+
+def kernel_ms(path, kernel):
+    for f in _files(path, "*kernel_stats.csv"):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Name"]:
+                return float(r["AverageNs"]) / 1e6, int(r["Calls"])
+    raise SystemExit(f"kernel {kernel!r} not in the kernel stats under {path}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--td", required=True)
+    ap.add_argument("--sq")
+    ap.add_argument("--lib", required=True)
+    ap.add_argument("-o", "--out", required=True)
+    a = ap.parse_args()
+    ms, calls = kernel_ms(a.trace, a.kernel)
+    f_kb, nf = counter(a.fetch, "FETCH_SIZE", a.kernel)
+    w_kb, nw = counter(a.write, "WRITE_SIZE", a.kernel)
+    gui, _ = counter(a.td, "GRBM_GUI_ACTIVE", a.kernel)
+    td, _ = counter(a.td, "TD_TD_BUSY_sum", a.kernel)
+    ta, _ = counter(a.td, "TA_BUSY_avr", a.kernel)
+    res = {"kernel": a.kernel, "kernel_ms": round(ms, 4), "trace_calls": calls, "pmc_launches": [nf, nw],
+           "fetch_size_kb_raw": f_kb, "write_size_kb_raw": w_kb,
+           "fetch_bytes_corrected": f_kb * 1024 * 2, "write_bytes": w_kb * 1024,
+           "hbm_bytes_per_launch": int(f_kb * 1024 * 2 + w_kb * 1024),
+           "hbm_GBs": round((f_kb * 2048 + w_kb * 1024) / (ms * 1e-3) / 1e9, 1),
+           "td_busy": round((td / 256) / (gui / 8), 4), "ta_busy": round(ta / (gui / 8), 4),
+           "correction": "FETCH_SIZE x2 (gfx950 64-B tally of 128-B requests); MALL hits included"}
+    if a.sq:
+        thr, _ = counter(a.sq, "SQ_THREAD_CYCLES_VALU", a.kernel)
+        act, _ = counter(a.sq, "SQ_ACTIVE_INST_VALU", a.kernel)
+        res["valu_lane_util"] = round(thr / (64 * act), 4)
+    with open(a.lib, "rb") as fh:
+        res["lib_sha256_16"] = hashlib.sha256(fh.read()).hexdigest()[:16]
+    with open(a.out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
