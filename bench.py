@@ -314,6 +314,11 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
                    "smooth_hits": int(wc.ref_smooth_hits), "pixels": int(wc.ref_pixels)}}
     r["executed"] = {"records": int(wc.records_fetched), "tri_tests": int(wc.tri_tests),
                      "normal_fetches": int(wc.normal_fetches), "pixels": int(wc.pixels)}
+    r["per_lane_record_loads"] = {
+        "lane_loads": int(wc.divergent_lane_loads), "distinct_records": int(wc.divergent_distinct_records),
+        "distinct_fraction": round(wc.divergent_distinct_records / max(1, wc.divergent_lane_loads), 4),
+        "what": "inner steps with the wave's lanes at more than one record (vector loads): lane loads vs "
+                "distinct records among the wave's lanes at that step"}
     r["simd_efficiency"] = {"closest": round(wc.lane_steps_closest / max(1, 64 * wc.wave_steps_closest), 3),
                             "shadow": round(wc.lane_steps_shadow / max(1, 64 * wc.wave_steps_shadow), 3)}
     r["lib_sha256_16"] = lib_sha

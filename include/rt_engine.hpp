@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -104,6 +105,24 @@ public:
         for (int32_t i = 0; i < desc.num_cameras; ++i) cams_.push_back(desc.cameras[i]);
         check(rt_scene_create(&desc, devices.empty() ? nullptr : devices.data(), (int32_t)devices.size(), &scene_));
     }
+    /* RayTracerEngine.init(from: url) / init(data:) (RayTracer.swift:30-49): the scene file is
+     * decoded by rt_scene_file_* (JSON or XML, ParsingKit's conventions), then built like the
+     * descriptor constructor.  Throws RenderError(RT_ERR_SCENE_FILE) on a decode error. */
+    static RayTracerEngine fromFile(const std::string& path, SceneFormat format = SceneFormat::Auto,
+                                    std::vector<int32_t> devices = {}) {
+        rt_scene_file* f = nullptr;
+        if (const int32_t rc = rt_scene_file_load(path.c_str(), fileFormat(format), &f))
+            throw RenderError(rc, rt_scene_file_last_error());
+        return fromSceneFile(f, std::move(devices));
+    }
+    static RayTracerEngine fromData(const std::string& data, SceneFormat format = SceneFormat::Auto,
+                                    const std::string& baseDir = "", std::vector<int32_t> devices = {}) {
+        rt_scene_file* f = nullptr;
+        if (const int32_t rc = rt_scene_file_parse(data.data(), data.size(), fileFormat(format),
+                                                   baseDir.empty() ? nullptr : baseDir.c_str(), &f))
+            throw RenderError(rc, rt_scene_file_last_error());
+        return fromSceneFile(f, std::move(devices));
+    }
     ~RayTracerEngine() { if (scene_) rt_scene_destroy(scene_); }
     RayTracerEngine(const RayTracerEngine&) = delete;
     RayTracerEngine& operator=(const RayTracerEngine&) = delete;
@@ -112,6 +131,24 @@ public:
     }
 
     rt_scene* handle() const { return scene_; }
+
+private:
+    static int32_t fileFormat(SceneFormat f) {
+        return f == SceneFormat::Json ? RT_SCENE_FORMAT_JSON : f == SceneFormat::Xml ? RT_SCENE_FORMAT_XML
+                                                                                     : RT_SCENE_FORMAT_AUTO;
+    }
+    static RayTracerEngine fromSceneFile(rt_scene_file* f, std::vector<int32_t> devices) {
+        std::unique_ptr<rt_scene_file, void (*)(rt_scene_file*)> own(f, rt_scene_file_destroy);
+        const rt_scene_desc* d = rt_scene_file_desc(f);
+        std::vector<CameraMeta> meta;
+        for (int32_t k = 0; k < d->num_cameras; ++k) {
+            const char* n = rt_scene_file_image_name(f, k);
+            meta.push_back(CameraMeta{"", n ? n : ""});
+        }
+        return RayTracerEngine(*d, std::move(devices), std::move(meta));
+    }
+
+public:
 
     CameraSpec cameraSpec(int32_t index) const {
         CameraSpec c;

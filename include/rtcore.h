@@ -19,6 +19,8 @@
  *   rt_render_device  <- same path, output left in device memory (bench / multi-GPU)
  *   rt_scene_info     <- RayTracerEngine.inspect / sceneMeshAndTriangleCounts
  *                                                          RayTracer/RayTracer.swift:52-67,208-227
+ *   rt_scene_file_*   <- SceneLoader.load (ParsingKit) in RayTracerEngine.init(from:data:)
+ *                                                          RayTracer/RayTracer.swift:30-49
  *   rt_ply_load       <- PLYLoader.load(from:)             RayTracer/Helpers/PLYReader.swift:54-210
  *                        (which drives CPly's ply_reader_* C ABI, CPly/include/PLYReaderWrapper.h:26-69)
  *
@@ -49,6 +51,7 @@ extern "C" {
 #define RT_ERR_INVALID_ARG     (-30)
 #define RT_ERR_UNSUPPORTED     (-31)  /* feature outside the implemented hot path      */
 #define RT_ERR_PLY             (-40)  /* PLYReader.swift:24-40 PlyError                */
+#define RT_ERR_SCENE_FILE      (-41)  /* SceneLoader / PKDecodingError (scene file decode) */
 #define RT_ERR_DEVICE          (-50)  /* HIP runtime failure                           */
 #define RT_ERR_OOM             (-51)
 #define RT_ERR_CANCELLED       (-60)  /* progress callback returned 0                  */
@@ -242,6 +245,9 @@ typedef struct rt_work_counters {
      * by lanes vs iterations run by their waves (64 x the max over the wave's lanes).     */
     int64_t lane_steps_closest, wave_steps_closest;
     int64_t lane_steps_shadow, wave_steps_shadow;
+    /* Vector-memory redundancy of the inner steps that take per-lane loads (the wave's lanes
+     * at more than one record): active lanes vs distinct records among them.             */
+    int64_t divergent_lane_loads, divergent_distinct_records;
 } rt_work_counters;
 int32_t rt_render_device_counted(rt_scene* scene, int32_t device_slot, int32_t camera_index,
                                  int32_t chunk_first, int32_t chunk_step,
@@ -259,6 +265,26 @@ typedef struct rt_ply_mesh {            /* PlyMesh (PLYReader.swift:14-19)      
 } rt_ply_mesh;
 int32_t rt_ply_load(const char* path, rt_ply_mesh* out);
 void    rt_ply_free(rt_ply_mesh* mesh);
+
+/* ---- scene files (host) --------------------------------------------------------
+ * RayTracerEngine.init(from: url) / init(data:)  RayTracer/RayTracer.swift:30-49, which read
+ * the scene through ParsingKit's SceneLoader.load(.url / .data(format:)) (SceneFormat
+ * Models/SceneFormat.swift:8-10).  The decoded scene owns every array rt_scene_file_desc()
+ * points into; pass that descriptor to rt_scene_create, then destroy the file.  JSON and XML
+ * follow ParsingKit's flexible conventions (myraytracer_amd/csrc/sceneio.cpp); a mesh's PLY
+ * path resolves against the scene file's directory (base_dir for in-memory data; NULL = the
+ * current directory).  Errors: RT_ERR_SCENE_FILE with rt_scene_file_last_error().           */
+#define RT_SCENE_FORMAT_AUTO  0
+#define RT_SCENE_FORMAT_JSON  1
+#define RT_SCENE_FORMAT_XML   2
+typedef struct rt_scene_file rt_scene_file;   /* opaque */
+int32_t rt_scene_file_load(const char* path, int32_t format, rt_scene_file** out);
+int32_t rt_scene_file_parse(const void* data, uint64_t size, int32_t format, const char* base_dir,
+                            rt_scene_file** out);
+const rt_scene_desc* rt_scene_file_desc(const rt_scene_file* file);
+const char* rt_scene_file_image_name(const rt_scene_file* file, int32_t camera_index);  /* Camera.imageName */
+const char* rt_scene_file_last_error(void);
+void    rt_scene_file_destroy(rt_scene_file* file);
 
 /* ---- debug / test hooks (not part of the reference surface) -------------------- */
 /* Canonical hash of instance `instance`'s BLAS (instance = -1: the TLAS); equal to the

@@ -61,6 +61,7 @@ class rt_scene_desc(C.Structure):
 
 
 RT_RENDER_FRAME_LAYOUT = 1
+RT_SCENE_FORMAT_AUTO, RT_SCENE_FORMAT_JSON, RT_SCENE_FORMAT_XML = 0, 1, 2
 
 
 class rt_stats(C.Structure):
@@ -83,7 +84,8 @@ class rt_work_counters(C.Structure):
                 ("ref_node_fetches", C.c_int64), ("ref_tri_tests", C.c_int64),
                 ("ref_smooth_hits", C.c_int64), ("ref_pixels", C.c_int64),
                 ("lane_steps_closest", C.c_int64), ("wave_steps_closest", C.c_int64),
-                ("lane_steps_shadow", C.c_int64), ("wave_steps_shadow", C.c_int64)]
+                ("lane_steps_shadow", C.c_int64), ("wave_steps_shadow", C.c_int64),
+                ("divergent_lane_loads", C.c_int64), ("divergent_distinct_records", C.c_int64)]
 
 
 class rt_ply_mesh(C.Structure):
@@ -103,6 +105,7 @@ RT_ERR_NO_RENDERER = -21
 RT_ERR_INVALID_ARG = -30
 RT_ERR_UNSUPPORTED = -31
 RT_ERR_PLY = -40
+RT_ERR_SCENE_FILE = -41
 RT_ERR_DEVICE = -50
 RT_ERR_OOM = -51
 RT_ERR_CANCELLED = -60
@@ -119,6 +122,8 @@ EXPORTED_SYMBOLS = [
     "rt_ply_load", "rt_ply_free", "rt_debug_bvh_hash", "rt_debug_host_build",
     "rt_debug_trace_rays", "rt_debug_occluded_rays", "rt_host_alloc", "rt_host_free", "rt_debug_wave_times",
     "rt_render_ex", "rt_host_register", "rt_host_unregister",
+    "rt_scene_file_load", "rt_scene_file_parse", "rt_scene_file_desc", "rt_scene_file_image_name",
+    "rt_scene_file_last_error", "rt_scene_file_destroy",
 ]
 
 
@@ -137,6 +142,18 @@ def bind(lib: C.CDLL) -> C.CDLL:
     lib.rt_render_ex.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, c_double_p, P(C.c_uint8),
                                  C.c_uint32, P(rt_stats), RT_PROGRESS_FN, C.c_void_p]
     lib.rt_render_ex.restype = C.c_int32
+    lib.rt_scene_file_load.argtypes = [C.c_char_p, C.c_int32, P(C.c_void_p)]
+    lib.rt_scene_file_load.restype = C.c_int32
+    lib.rt_scene_file_parse.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_char_p, P(C.c_void_p)]
+    lib.rt_scene_file_parse.restype = C.c_int32
+    lib.rt_scene_file_desc.argtypes = [C.c_void_p]
+    lib.rt_scene_file_desc.restype = P(rt_scene_desc)
+    lib.rt_scene_file_image_name.argtypes = [C.c_void_p, C.c_int32]
+    lib.rt_scene_file_image_name.restype = C.c_char_p
+    lib.rt_scene_file_last_error.argtypes = []
+    lib.rt_scene_file_last_error.restype = C.c_char_p
+    lib.rt_scene_file_destroy.argtypes = [C.c_void_p]
+    lib.rt_scene_file_destroy.restype = None
     lib.rt_host_register.argtypes = [C.c_void_p, C.c_uint64]
     lib.rt_host_register.restype = C.c_int32
     lib.rt_host_unregister.argtypes = [C.c_void_p]

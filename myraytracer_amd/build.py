@@ -17,7 +17,7 @@ PKG = os.path.join(ROOT, "myraytracer_amd")
 CSRC = os.path.join(PKG, "csrc")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
-PRODUCT_SOURCES = ["render.hip", "wavefront.hip", "scene.cpp", "ply.cpp"]
+PRODUCT_SOURCES = ["render.hip", "wavefront.hip", "scene.cpp", "ply.cpp", "sceneio.cpp"]
 # -ffp-contract=off on host AND device: the reference does no FMA contraction
 COMMON_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
 

@@ -137,9 +137,15 @@ constexpr int kSpill = kStackCap - kLds;   // the host refuses deeper scenes (sc
 static_assert(kSpill > 0, "LDS part larger than the stack");
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 typedef __attribute__((address_space(5))) unsigned long long priv_u64;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f32x4 lds_crec;   // a CRec = 4 consecutive f32x4
+typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
 struct Stack {
     lds_u64* lds;        // &lds_base[threadIdx.x]; stride blockDim.x (MYRT_STRIDE64: per-wave slab, stride 64)
     priv_u64* spill;     // kSpill private entries
+    const lds_crec* top; // this wave's LDS copy of compact records [0, top_n) (render kernels)
+    int top_n;           // 0 = no LDS records
 #if MYRT_STRIDE64
     static constexpr int stride = 64;
 #else
@@ -198,7 +204,26 @@ struct Stack {
     Stack name;                                                      \
     MYRT_STACK_LDS(name, lds_base);                                  \
     name.spill = (priv_u64*)(name##_spill_mem);                      \
+    name.top = nullptr;                                              \
+    name.top_n = 0;                                                  \
     name.sp = 0
+
+// Copy compact records [0, n) into this wave's LDS slab (n <= kLdsTopMax), for Stack::top.  Every lane copies records lane, lane+64, ...; LDS operations of one wave
+// complete in order, so the wave's later reads see them (the barrier orders the waves of
+// multi-wave blocks, which each copy their own slab).
+// Called by every lane of the block (it holds a barrier); the slabs follow the stacks.
+__device__ __forceinline__ const lds_crec* stage_top_records(const RenderParams& P, unsigned long long* lds_base) {
+    const int n = P.lds_top_n;
+    if (n <= 0) return nullptr;
+    lds_crec* slab = (lds_crec*)(lds_u64*)(lds_base + (size_t)blockDim.x * kLds) + (size_t)(threadIdx.x >> 6) * n * 4;
+    const f32x4* src = reinterpret_cast<const f32x4*>(P.crecs);
+    for (int k = threadIdx.x & 63; k < n; k += 64) {
+        const f32x4 a = src[4 * k], b = src[4 * k + 1], c = src[4 * k + 2], d = src[4 * k + 3];
+        slab[4 * k] = a; slab[4 * k + 1] = b; slab[4 * k + 2] = c; slab[4 * k + 3] = d;
+    }
+    __syncthreads();
+    return slab;
+}
 
 // Work counters (COUNT instantiations only).  recs/tris/normals/insts = work this kernel
 // executed.  With RenderParams::count_ref set, the COUNT walk instead follows the
@@ -210,6 +235,7 @@ struct Counts {
     unsigned long long recs, tris, normals, insts, nodes, smooth;
     unsigned long long it_closest, it_shadow;   // loop iterations of this lane (divergence study)
     unsigned shadow_traced;                     // shadow rays whose any-hit walk ran (<= shadow)
+    unsigned long long div_lanes, div_distinct; // per-lane inner steps / of them, first lane of its record
 };
 constexpr int kMissRef = 0x7fffffff;   // count_ref any-hit: a pushed child whose slab test missed
 
@@ -506,6 +532,31 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
         const SRec R = load_rec_scalar(P.recs + r0);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
 #endif
+    }
+    if (COUNT && !P.count_ref) {             // redundancy of the per-lane loads below
+        unsigned long long left = __ballot(1);
+        int my_leader = -1;
+        while (left) {                       // one group of equal refs per iteration
+            const int leader = __builtin_ctzll(left);
+            const int r = __shfl(ref, leader, 64);
+            if (ref == r) my_leader = leader;
+            left &= ~__ballot(ref == r);
+        }
+        c.div_lanes += 1;
+        c.div_distinct += ((int)(threadIdx.x & 63) == my_leader) ? 1 : 0;
+    }
+    if (ref < st.top_n) {                    // near-root record: this wave's LDS copy
+        const lds_crec* q = st.top + 4 * ref;
+        const f32x4 a = q[0], b = q[1], e = q[2];
+        // the refs are read as integers: bit-casting elements of a float vector read every
+        // element as element 0 (the same miscompile as the SGPR-tuple case, load_crec_scalar)
+        const i32x4 f = *(const lds_i32x4*)(q + 3);
+        CRec R;
+        R.lo[0][0] = a.x; R.lo[0][1] = a.y; R.lo[0][2] = a.z; R.lo[1][0] = a.w;
+        R.lo[1][1] = b.x; R.lo[1][2] = b.y; R.hi[0][0] = b.z; R.hi[0][1] = b.w;
+        R.hi[0][2] = e.x; R.hi[1][0] = e.y; R.hi[1][1] = e.z; R.hi[1][2] = e.w;
+        R.ref[0] = f.x; R.ref[1] = f.y;
+        return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
     }
     if (ref < P.compact_limit) {
 #if MYRT_CREC56

@@ -138,6 +138,7 @@ struct RenderParams {
     int32_t scalar_nodes;            // wave-uniform records via scalar loads (device.h inner_step)
     int32_t compact_limit;           // records below this index are read from crecs
     int32_t rot_slots;               // megakernel dispatch order: selected chunk rows rotated by this many
+    int32_t lds_top_n;               // megakernel: compact records [0, n) served from LDS (0 = off)
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)
@@ -159,5 +160,9 @@ constexpr int kMaxDepthGPU = 16;     // mirror/conductor recursion levels kept p
 // The reference gives the TLAS walk and each BLAS walk their own 64-entry stacks
 // (RTContext.swift:550, 623); one shared stack of 128 holds both at their limits.
 constexpr int kStackCap = 128;
+
+// Breadth-first record prefix of the first BLAS that the render kernels copy into LDS at
+// wave start (device.h Stack::top): the near-root levels every ray walks.
+constexpr int kLdsTopMax = 127;
 
 }  // namespace myrt

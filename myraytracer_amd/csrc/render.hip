@@ -173,8 +173,11 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     const DCamera& C = P.cam;
     const bool valid = (i < C.width) && (j < C.height);
     Counts cnt{};
+    const lds_crec* top = stage_top_records(P, lds_stack);
     if (valid) {
         MYRT_STACK(st, lds_stack);
+        st.top = top;
+        st.top_n = P.lds_top_n;
         PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
         V3 pixel = v3(0, 0, 0);
         const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
@@ -264,6 +267,10 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
         if (lane == 0 && !P.count_ref) {
             atomicAdd(&P.counters[9], lc); atomicAdd(&P.counters[10], wc);
             atomicAdd(&P.counters[11], ls); atomicAdd(&P.counters[12], ws);
+        }
+        const unsigned long long dl = wave_sum(cnt.div_lanes), dd2 = wave_sum(cnt.div_distinct);
+        if (lane == 0 && !P.count_ref && dl) {
+            atomicAdd(&P.counters[14], dl); atomicAdd(&P.counters[15], dd2);
         }
     }
 }
@@ -513,6 +520,16 @@ extern "C" int32_t rt_rows_for_chunks(int32_t height, int32_t chunk_first, int32
     return rows;
 }
 
+static int32_t env_int(const char* name, int32_t def, int32_t lo, int32_t hi) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return def;
+    return std::min(hi, std::max(lo, (int32_t)std::atoi(v)));
+}
+
+// Near-root BLAS records kept in LDS per wave (device.h stage_top_records): 31 = the top 5
+// levels; with the 16-entry LDS stack a wave then holds 10 KB, 16 waves fill 160 KB.
+constexpr int32_t kLdsTopDefault = 31;
+
 // Absolute pruning margin for rays whose origins lie within `origin_dist` of the scene
 // center (or inside the scene bounds): prune_k * (|o - v0| + t|d|) with both terms bounded
 // by the origin's distance plus the scene diagonal (scene.cpp, "pruning margin").
@@ -586,6 +603,9 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         P.compact_limit = (ce && ce[0] == '0') ? 0 : (int32_t)S.compact_records;
         const char* te = std::getenv("MYRT_CTRI");              // A/B switch: MYRT_CTRI=0
         P.ctris = (S.compact_tris && !(te && te[0] == '0')) ? r.ctris : nullptr;
+        // near-root records in LDS (megakernel; launch() clears it for the other kernels)
+        P.lds_top_n = (int32_t)std::min<int64_t>(env_int("MYRT_LDS_TOP", kLdsTopDefault, 0, kLdsTopMax),
+                                                 std::min<int64_t>(S.lds_top_records, P.compact_limit));
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
@@ -665,7 +685,7 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     const int bt = block_threads();
     dim3 grid = render_grid(P, bt);
     dim3 block((unsigned)bt, 1, 1);
-    const size_t lds = (size_t)dev::kLds * bt * sizeof(int2);
+    const size_t lds = (size_t)dev::kLds * bt * sizeof(int2) + (size_t)(bt / 64) * P.lds_top_n * sizeof(CRec);
     const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
     // the unified walk needs an identity scene; reference-order counting uses the general walk
     const char* ue = std::getenv("MYRT_UNIFIED");
@@ -817,18 +837,13 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
         out->ref_smooth_hits = (int64_t)q[8]; out->ref_pixels = (int64_t)q[6];
         out->lane_steps_closest = (int64_t)c[9]; out->wave_steps_closest = (int64_t)c[10];
         out->lane_steps_shadow = (int64_t)c[11]; out->wave_steps_shadow = (int64_t)c[12];
+        out->divergent_lane_loads = (int64_t)c[14]; out->divergent_distinct_records = (int64_t)c[15];
     }
     return RT_OK;
 }
 
 // True when [p, p+bytes) lies inside ONE page-locked host allocation (hipHostMalloc /
 // hipHostRegister): the DMA engine can then write it directly.  NULL counts as true.
-static int32_t env_int(const char* name, int32_t def, int32_t lo, int32_t hi) {
-    const char* v = std::getenv(name);
-    if (!v || !*v) return def;
-    return std::min(hi, std::max(lo, (int32_t)std::atoi(v)));
-}
-
 static bool pinned_range(const void* p, size_t bytes) {
     if (!p || bytes == 0) return true;
     const void* ends[2] = {p, static_cast<const char*>(p) + bytes - 1};

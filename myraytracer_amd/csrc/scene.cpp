@@ -392,20 +392,38 @@ struct InstBuild { int blas; double M[16]; int material; D3 motion; double wlo[3
 // preorder (near-left first); each leaf's primitives become a contiguous run of
 // entries produced by `emit_leaf(first_prim_slot, count)` which returns the index of
 // the run's first entry.  Returns the root ref.
+// With topRecords > 0 the first min(topRecords, inner nodes) records are the inner nodes
+// nearest the root in breadth-first order (the kernels keep that prefix in LDS, device.h
+// Stack::top); the rest follow in preorder.  Record numbering is free: traversal order
+// depends only on the tree.
 template <class EmitLeaf>
-static int32_t layout_bvh(const RefBVH& b, std::vector<WRec>& recs, EmitLeaf emit_leaf) {
+static int32_t layout_bvh(const RefBVH& b, std::vector<WRec>& recs, EmitLeaf emit_leaf, int64_t topRecords = 0) {
     if (b.isLeaf(0) || (b.count[0] == 0 && b.nodesUsed == 0)) {
         const int64_t first = emit_leaf(b.leftFirst[0], b.count[0]);
         return ~(int32_t)first;
     }
-    // assign record ids in preorder
     std::vector<int64_t> recOf(b.leftFirst.size(), -1);
     std::vector<int64_t> order;
+    if (topRecords > 0) {                                  // breadth-first prefix
+        recOf[0] = (int64_t)recs.size();
+        order.push_back(0);
+        for (size_t q = 0; q < order.size() && (int64_t)order.size() < topRecords; ++q) {
+            const int64_t i = order[q];
+            for (int64_t c : {b.leftFirst[i], b.leftFirst[i] + 1}) {
+                if (b.isLeaf(c) || (int64_t)order.size() >= topRecords) continue;
+                recOf[c] = (int64_t)recs.size() + (int64_t)order.size();
+                order.push_back(c);
+            }
+        }
+    }
+    // the rest in preorder
     std::vector<int64_t> st{0};
     while (!st.empty()) {
         int64_t i = st.back(); st.pop_back();
-        recOf[i] = (int64_t)recs.size() + (int64_t)order.size();
-        order.push_back(i);
+        if (recOf[i] < 0) {
+            recOf[i] = (int64_t)recs.size() + (int64_t)order.size();
+            order.push_back(i);
+        }
         const int64_t L = b.leftFirst[i], R = L + 1;
         if (!b.isLeaf(R)) st.push_back(R);
         if (!b.isLeaf(L)) st.push_back(L);
@@ -741,7 +759,10 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             return first;
         };
         bb.tri_first = (int64_t)S.tris.size();
-        bb.root_ref = layout_bvh(bb.bvh, S.recs, emit);
+        // the first BLAS starts at record 0: its top records form the LDS-resident prefix
+        const int64_t top = S.recs.empty() ? kLdsTopMax : 0;
+        bb.root_ref = layout_bvh(bb.bvh, S.recs, emit, top);
+        if (top > 0) S.lds_top_records = std::min<int64_t>(kLdsTopMax, (int64_t)S.recs.size());
         bb.tri_end = (int64_t)S.tris.size();
         for (int k = 0; k < 3; ++k) { bb.root_lo[k] = bb.bvh.lo[k]; bb.root_hi[k] = bb.bvh.hi[k]; }
         bb.bvh = RefBVH();   // free host copy

@@ -22,6 +22,7 @@ typedef struct oracle_stats {
     int64_t node_fetches, tri_tests, smooth_hits, pixels;
     double milliseconds;
     int32_t threads;
+    int64_t shadow_rays_used;
 } oracle_stats;
 int32_t oracle_scene_create(const rt_scene_desc* desc, void** out);
 void oracle_scene_destroy(void* s);
@@ -141,9 +142,9 @@ static void scene_grid(SceneData& s) {
     s.finish(V(8, 12, 20), V(20, 20, 20), 4);
 }
 
-static void compare_with_oracle(const SceneData& s, const myrt::RenderResult& r, int cam, const char* what) {
+static void compare_with_oracle(const rt_scene_desc& desc, const myrt::RenderResult& r, int cam, const char* what) {
     void* o = nullptr;
-    EXPECT(oracle_scene_create(&s.desc, &o) == RT_OK, "%s: oracle scene", what);
+    EXPECT(oracle_scene_create(&desc, &o) == RT_OK, "%s: oracle scene", what);
     const size_t px = (size_t)r.camera.width * r.camera.height;
     std::vector<double> ref(px * 3);
     std::vector<uint8_t> ref8(px * 4);
@@ -163,7 +164,34 @@ static void compare_with_oracle(const SceneData& s, const myrt::RenderResult& r,
                 (long long)r.stats.secondary_rays);
 }
 
+// The C1 scene as a scene file (RayTracerEngine.init(data:), RayTracer.swift:35-36)
+static const char* kC1Json = R"({"Scene": {
+  "MaxRecursionDepth": "6", "BackgroundColor": "10 20 30", "ShadowRayEpsilon": "1e-3",
+  "IntersectionTestEpsilon": "1e-6",
+  "Cameras": {"Camera": {"_id": "1", "_type": "lookAt", "Position": "0 0 0", "GazePoint": "0 0 -1",
+              "Up": "0 1 0", "FovY": "60", "NearDistance": "1", "ImageResolution": "80 60",
+              "ImageName": "c1_file.png"}},
+  "Lights": {"AmbientLight": "25 25 25", "PointLight": {"_id": "1", "Position": "2 2 0", "Intensity": "3e3 3e3 3e3"}},
+  "Materials": {"Material": {"_id": "1", "AmbientReflectance": "1 1 1", "DiffuseReflectance": "0.8 0.5 0.3",
+                "SpecularReflectance": "0.5 0.5 0.5", "PhongExponent": "32"}},
+  "VertexData": "-1 -1 -3 1 -1 -3 0 1 -3",
+  "Objects": {"Mesh": {"_id": "1", "_shadingMode": "flat", "Material": "1", "Faces": "1 2 3"}}}})";
+
 static int run_cpu() {
+    // scene files: a decode error is RT_ERR_SCENE_FILE; a good file then needs the device
+    try {
+        auto e = myrt::RayTracerEngine::fromData("{\"Scene\": {\"BackgroundColor\": \"1 2\"}}");
+        EXPECT(false, "bad scene file accepted");
+    } catch (const myrt::RenderError& e) {
+        EXPECT(e.code == RT_ERR_SCENE_FILE && std::string(e.what()).find("requires 3") != std::string::npos,
+               "code %d (%s)", e.code, e.what());
+    }
+    try {
+        auto e = myrt::RayTracerEngine::fromData(kC1Json);
+        EXPECT(false, "scene creation succeeded without a GPU");
+    } catch (const myrt::RenderError& e) {
+        EXPECT(e.code == RT_ERR_DEVICE, "code %d (%s)", e.code, e.what());
+    }
     SceneData s;
     scene_c1(s, 32, 32);
     try {
@@ -195,7 +223,7 @@ static int run_gpu() {
         EXPECT(r.fileName == "c1.png" && r.camera.width == 96 && r.camera.height == 64, "camera spec");
         EXPECT(!seen.empty() && seen.back() == 1.0, "progress did not reach 1");
         for (size_t i = 1; i < seen.size(); ++i) EXPECT(seen[i] >= seen[i - 1], "progress not monotone");
-        compare_with_oracle(s, r, 0, "c1");
+        compare_with_oracle(s.desc, r, 0, "c1");
         const auto info = eng.inspect();
         EXPECT(info.meshes == 1 && info.triangles == 1 && info.cameras.size() == 1, "inspect");
         // invalid camera index -> NSError code -10 (RayTracer.swift:151-154)
@@ -218,6 +246,15 @@ static int run_gpu() {
         myrt::check(rt_render(eng.handle(), 0, 0, 1, pin.data(), nullptr, &st, nullptr, nullptr));
         EXPECT(std::memcmp(pin.data(), r.rgb.data(), r.rgb.size() * sizeof(double)) == 0, "pinned output differs");
     }
+    {   // a scene file decoded by the library (RayTracerEngine.init(data:)) renders like its descriptor
+        auto eng = myrt::RayTracerEngine::fromData(kC1Json, myrt::SceneFormat::Json);
+        auto r = eng.render(myrt::SceneFormat::Auto, 0);
+        EXPECT(r.fileName == "c1_file.png" && r.camera.width == 80 && r.camera.height == 60, "file camera spec");
+        rt_scene_file* f = nullptr;
+        myrt::check(rt_scene_file_parse(kC1Json, std::strlen(kC1Json), RT_SCENE_FORMAT_AUTO, nullptr, &f));
+        compare_with_oracle(*rt_scene_file_desc(f), r, 0, "c1 scene file");
+        rt_scene_file_destroy(f);
+    }
     {   // two cameras (lookAt + nearPlane with 4 spp), mirror bounces, renderAll
         SceneData s;
         scene_grid(s);
@@ -231,8 +268,8 @@ static int run_gpu() {
             return true;
         });
         EXPECT(all.size() == 2 && !msgs.empty() && msgs.back() == "Done" && last == 1.0, "renderAll progress");
-        compare_with_oracle(s, all[0], 0, "grid cam0");
-        compare_with_oracle(s, all[1], 1, "grid cam1 (nearPlane, 4 spp)");
+        compare_with_oracle(s.desc, all[0], 0, "grid cam0");
+        compare_with_oracle(s.desc, all[1], 1, "grid cam1 (nearPlane, 4 spp)");
         EXPECT(all[0].stats.secondary_rays > 0, "no mirror bounces traced");
         const auto info = eng.inspect();
         EXPECT(info.meshes == 2 && info.triangles == 2 * 40 * 40 + 12, "inspect triangles %lld",

@@ -76,7 +76,7 @@ def main():
            "td_busy": round((td / 256) / (gui / 8), 4), "ta_busy": round(ta / (gui / 8), 4),
            "correction": "FETCH_SIZE x2 (gfx950 64-B tally of 128-B requests); MALL hits included"}
     if a.sq:
-        thr, _ = counter(a.sq, "SQ_THREAD_CYCLES_VALU", a.kernel)
+        thr, _ = counter(a.td, "SQ_THREAD_CYCLES_VALU", a.kernel)
         act, _ = counter(a.sq, "SQ_ACTIVE_INST_VALU", a.kernel)
         res["valu_lane_util"] = round(thr / (64 * act), 4)
     with open(a.lib, "rb") as fh:
