@@ -82,6 +82,9 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                     const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
                     contrib = (Ld + Ls) * atten;
                 }
+                // pin it here: otherwise the compiler sinks the whole computation below the
+                // walk, into the one branch that uses it, and spills its inputs across the walk
+                asm volatile("" : "+v"(contrib.x), "+v"(contrib.y), "+v"(contrib.z));
                 if (NdotL > 0 || MYRT_REF(P)) {
                     c.shadow_traced++;
                     const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
@@ -136,6 +139,15 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 #ifndef MYRT_MEGA_WPE
 #define MYRT_MEGA_WPE 4      // amdgpu_waves_per_eu for the megakernel (0 = compiler default = 2 waves at ~200 VGPRs)
 #endif
+#ifndef MYRT_PIXLDS
+#define MYRT_PIXLDS 1        // pixel sum + PCG32 state kept in LDS across the walks (not spilled)
+#endif
+// Per-pixel PCG32 seed (Object+Extension.swift:294)
+__device__ __forceinline__ unsigned long long pixel_seed(int i, int j) {
+    return (((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull;
+}
+constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;   // x, y, z, rng.state (8 B x 64 lanes each)
+typedef __attribute__((address_space(3))) double lds_f64;
 #if MYRT_MEGA_WPE > 0
 #define MYRT_MEGA_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_MEGA_WPE)))
 #else
@@ -174,11 +186,16 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     const bool valid = (i < C.width) && (j < C.height);
     Counts cnt{};
     const lds_crec* top = stage_top_records(P, lds_stack);
+#if MYRT_PIXLDS
+    // this wave's [kPixSlots][64] slab after the stacks and the near-root records
+    lds_f64* pacc = (lds_f64*)(lds_u64*)(lds_stack + (size_t)blockDim.x * kLds +
+                                         (size_t)(blockDim.x >> 6) * P.lds_top_n * 8) + wave * (kPixSlots * 64) + lane;
+#endif
     if (valid) {
         MYRT_STACK(st, lds_stack);
         st.top = top;
         st.top_n = P.lds_top_n;
-        PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
+        PCG32 rng(pixel_seed(i, j));
         V3 pixel = v3(0, 0, 0);
         const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
         const int n = C.n;
@@ -189,8 +206,18 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                 const double xi2 = rng.nextFloat();
                 const double iOffset = ((double)sx + xi1) / (double)n;
                 const double jOffset = ((double)sy + xi2) / (double)n;
-                const double currentI = (double)i + iOffset;
-                const double currentJ = (double)j + jOffset;
+#if MYRT_PIXLDS
+                // per-sample copies the compiler cannot hoist: otherwise (double)i, (double)j and
+                // eye - w*nd are computed once before the sample loop and spilled across the walks
+                int ii = i, jj = j;
+                double nd = C.nd;
+                asm volatile("" : "+v"(ii), "+v"(jj), "+v"(nd));
+#else
+                const int ii = i, jj = j;
+                const double nd = C.nd;
+#endif
+                const double currentI = (double)ii + iOffset;
+                const double currentJ = (double)jj + jOffset;
                 const V3 vOff = v * (currentJ * C.dv);
                 const V3 rowTopLeft = q00 - vOff;
                 const V3 uOff = u * (currentI * C.du);
@@ -211,14 +238,35 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                 }
                 const double time = rng.nextFloat();
                 const double denom = dot(dir, w);
-                const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
+                const double tImg = dot((eye - w * nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
                 const double tlo = smax(tImg, 0.0);
+#if MYRT_PIXLDS
+                // The pixel sum and (when the walk does not draw from it) the PCG32 state wait
+                // in LDS while the rays are traced, so they are not live - spilled - across the
+                // walks; the memory clobber makes the reloads real loads.
+                if (!BOUNCE) pacc[3 * 64] = __builtin_bit_cast(double, rng.state);
+                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt);
+                asm volatile("" ::: "memory");
+                if (!BOUNCE) {
+                    rng.state = __builtin_bit_cast(unsigned long long, (double)pacc[3 * 64]);
+                    rng.inc = (pixel_seed(i, j) << 1) | 1ull;     // PCG32(seed) sets inc = seed<<1 | 1
+                }
+                if (sampleIndex == 0) {
+                    pacc[0] = 0.0 + col.x; pacc[64] = 0.0 + col.y; pacc[128] = 0.0 + col.z;
+                } else {
+                    pacc[0] = pacc[0] + col.x; pacc[64] = pacc[64] + col.y; pacc[128] = pacc[128] + col.z;
+                }
+#else
                 const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt);
                 pixel = pixel + col;
+#endif
                 sampleIndex += 1;
                 if (sampleIndex >= C.samples) break;
             }
         }
+#if MYRT_PIXLDS
+        pixel = v3(pacc[0], pacc[64], pacc[128]);
+#endif
         const V3 px = pixel / (double)C.samples;
         const size_t row = out_row_of(P, chunk, rowInChunk);
         const size_t o = row * (size_t)C.width + i;
@@ -528,7 +576,7 @@ static int32_t env_int(const char* name, int32_t def, int32_t lo, int32_t hi) {
 
 // Near-root BLAS records kept in LDS per wave (device.h stage_top_records): 31 = the top 5
 // levels; with the 16-entry LDS stack a wave then holds 10 KB, 16 waves fill 160 KB.
-constexpr int32_t kLdsTopDefault = 31;
+constexpr int32_t kLdsTopDefault = 0;    // measured no gain; its LDS now holds the pixel sums
 
 // Absolute pruning margin for rays whose origins lie within `origin_dist` of the scene
 // center (or inside the scene bounds): prune_k * (|o - v0| + t|d|) with both terms bounded
@@ -685,7 +733,8 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     const int bt = block_threads();
     dim3 grid = render_grid(P, bt);
     dim3 block((unsigned)bt, 1, 1);
-    const size_t lds = (size_t)dev::kLds * bt * sizeof(int2) + (size_t)(bt / 64) * P.lds_top_n * sizeof(CRec);
+    const size_t lds = (size_t)dev::kLds * bt * sizeof(int2) + (size_t)(bt / 64) * P.lds_top_n * sizeof(CRec) +
+                       (size_t)dev::kPixSlots * bt * sizeof(double);
     const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
     // the unified walk needs an identity scene; reference-order counting uses the general walk
     const char* ue = std::getenv("MYRT_UNIFIED");
