@@ -298,10 +298,12 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
         r["traffic_source"] = os.path.relpath(ppath, ROOT)
         r["profile_build_matches"] = prof.get("lib_sha256_16") == lib_sha
         r["binding"] = {
-            "resource": "vector-memory data path (TA/TD): per-lane BVH record and triangle loads served from L1/L2",
+            "resource": "VALU issue (FP64 slab/Moeller-Trumbore arithmetic at ~half lane utilisation), with the "
+                        "vector-memory data path (TA/TD) next: per-lane BVH record and triangle loads served from L1/L2",
+            "valu_busy": prof.get("valu_busy"), "valu_lane_util": prof.get("valu_lane_util"),
             "td_busy": prof.get("td_busy"), "ta_busy": prof.get("ta_busy"),
-            "valu_lane_util": prof.get("valu_lane_util"),
-            "note": "td_busy = TD_TD_BUSY_sum/256 / (GRBM_GUI_ACTIVE/8) from the same profile",
+            "note": "valu_busy = SQ_ACTIVE_INST_VALU/256 CUs / (GRBM_GUI_ACTIVE/8) (rocprofiler-sdk VALUBusy); "
+                    "td_busy = TD_TD_BUSY_sum/256 / (GRBM_GUI_ACTIVE/8); both from the same profile",
             "executed_load_bytes": int(load_bytes),
             "executed_load_GBs": round(load_bytes / (kernel_ms * 1e-3) / 1e9, 1)}
     r["reference_work"] = {

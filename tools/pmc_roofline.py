@@ -12,6 +12,7 @@ Per launch (median over the dispatches of that kernel):
       return) path utilisation - the resource that binds this kernel.
   ta_busy  = TA_BUSY_avr / (GRBM_GUI_ACTIVE / 8).
   valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)  (needs --sq).
+  valu_busy = SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8)  (rocprofiler-sdk's VALUBusy).
   kernel_ms = average duration from the --kernel-trace --stats pass.
 lib_sha256_16 ties the summary to the library build it measured (bench.py checks it).
 """
@@ -79,6 +80,9 @@ def main():
         thr, _ = counter(a.td, "SQ_THREAD_CYCLES_VALU", a.kernel)
         act, _ = counter(a.sq, "SQ_ACTIVE_INST_VALU", a.kernel)
         res["valu_lane_util"] = round(thr / (64 * act), 4)
+        # VALUBusy (rocprofiler-sdk derived counter for gfx950): SQ_ACTIVE_INST_VALU counts
+        # quad-cycles per CU summed over its 4 SIMDs -> fraction of cycles the SIMDs issue VALU
+        res["valu_busy"] = round(act / 256 / (gui / 8), 4)
     with open(a.lib, "rb") as fh:
         res["lib_sha256_16"] = hashlib.sha256(fh.read()).hexdigest()[:16]
     with open(a.out, "w") as fh:
