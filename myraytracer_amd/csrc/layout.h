@@ -145,6 +145,11 @@ struct RenderParams {
     long long* events;               // k_events output: per-pixel area-light evaluations
     int32_t num_alights;
     int32_t has_special;             // spheres / planes present (general walk tests kinds)
+    // maxRecursionDepth > kMaxDepthGPU (render_full<.., DEEP>): trace() levels beyond the
+    // per-lane private frames live in `deep`, [level - kMaxDepthGPU - 1][lane of the launch];
+    // a launch covers selected chunks [slot_base, slot_base + gridDim.x / tiles-per-chunk)
+    void* deep;
+    int32_t slot_base;
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
     unsigned long long* counters;    // [0] shadow rays cast, [1] secondary rays, [2..12] work counters,
@@ -154,7 +159,8 @@ struct RenderParams {
 
 constexpr int kCounterWords = 16;   // u64 words behind RenderParams::counters
 constexpr int kCounterShadowTraced = 13;
-constexpr int kMaxDepthGPU = 16;     // mirror/conductor recursion levels kept per lane
+constexpr int kMaxDepthGPU = 16;     // trace() levels kept in private memory per lane (deeper: RenderParams::deep)
+constexpr int64_t kDeepBytesCap = 8ll << 30;   // device bytes of deep frames per launch batch
 
 // Per-lane traversal stack capacity (device.h Stack: kLds LDS entries + the private rest).
 // The reference gives the TLAS walk and each BLAS walk their own 64-entry stacks

@@ -405,6 +405,7 @@ struct DeviceReplica {
     long long* events = nullptr;              // area-light passes (grown on demand)
     long long* jstart = nullptr;
     int64_t cap_px = 0;
+    void* deep = nullptr; int64_t deep_cap = 0;   // deep trace() frames (render_full<.., true>)
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     unsigned long long* wave_times = nullptr; int64_t wave_times_cap = 0;   // rt_debug_wave_times
     hipStream_t stream = nullptr;
@@ -442,6 +443,7 @@ static void free_replica(DeviceReplica& r) {
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart); (void)hipFree(r.wave_times);
+    (void)hipFree(r.deep);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -552,9 +554,24 @@ static DCamera camera_constants(const rt_camera& cam) {
     return C;
 }
 
+static int block_threads();
+// Device bytes of deep frames per launch batch (MYRT_DEEP_CAP_MB overrides, for tests)
+static double deep_cap() {
+    const char* e = std::getenv("MYRT_DEEP_CAP_MB");
+    return (e && *e) ? std::max(1.0, std::atof(e)) * 1048576.0 : (double)kDeepBytesCap;
+}
+// Lanes of one selected 8-row chunk (render_grid) times the deep trace() levels per lane.
+static double deep_bytes_per_chunk(int32_t max_depth, int32_t width) {
+    const int bt = block_threads(), px = 8 * (bt / 64);
+    const double lanes = (double)((std::max(1, width) + px - 1) / px) * bt;
+    return lanes * (double)std::max(0, max_depth - kMaxDepthGPU) * (double)sizeof(dev::Frame);
+}
 static int32_t check_renderable(const HostScene& S, int32_t cam) {
     if (cam < 0 || cam >= (int32_t)S.cams.size()) return fail(RT_ERR_INVALID_CAMERA, "Invalid camera index");
-    if (S.max_depth > kMaxDepthGPU) return fail(RT_ERR_UNSUPPORTED, "maxRecursionDepth above the GPU limit");
+    // trace() levels beyond kMaxDepthGPU live in a device buffer, one Frame per level and lane
+    // of a launch batch (render_full<.., DEEP>); one 8-row chunk's lanes must fit kDeepBytesCap
+    if (S.max_depth > kMaxDepthGPU && deep_bytes_per_chunk(S.max_depth, S.cams[cam].width) > deep_cap())
+        return fail(RT_ERR_UNSUPPORTED, "maxRecursionDepth too deep for the device frame buffer");
     return RT_OK;
 }
 
@@ -693,9 +710,24 @@ static dim3 render_grid(const RenderParams& P, int threads) {
 
 static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count) {
     const int bt = block_threads();
-    dim3 grid = render_grid(P, bt);
     dim3 block((unsigned)bt, 1, 1);
     const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long);
+    const unsigned per_slot = render_grid(P, bt).x / (unsigned)std::max(1, P.num_chunks);   // blocks per chunk
+    // maxRecursionDepth > kMaxDepthGPU: batches of chunks whose deep frames fit kDeepBytesCap
+    const bool deep = P.max_depth > kMaxDepthGPU;
+    int32_t batch = P.num_chunks;
+    if (deep) {
+        const double per_chunk = deep_bytes_per_chunk(P.max_depth, P.cam.width);
+        batch = (int32_t)std::max(1.0, std::min((double)P.num_chunks, std::floor(deep_cap() / per_chunk)));
+        const int64_t need = (int64_t)(per_chunk * batch);
+        if (need > r.deep_cap) {
+            (void)hipFree(r.deep);
+            r.deep = nullptr; r.deep_cap = 0;
+            if (hipMalloc(&r.deep, need) != hipSuccess) return fail(RT_ERR_OOM, "device allocation of deep trace() frames failed");
+            r.deep_cap = need;
+        }
+        P.deep = r.deep;
+    }
     if (P.num_alights > 0) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
         if (px > r.cap_px) {
@@ -708,20 +740,34 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
         }
         P.events = r.events;
         P.jstart = r.jstart;
-        hipLaunchKernelGGL(dev::k_events, grid, block, lds, stream, P);
+        for (int32_t base = 0; base < P.num_chunks; base += batch) {
+            P.slot_base = base;
+            dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);
+            if (deep) hipLaunchKernelGGL((dev::k_events<true>), grid, block, lds, stream, P);
+            else hipLaunchKernelGGL((dev::k_events<false>), grid, block, lds, stream, P);
+        }
         hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), dim3(256, 1, 1), 0, stream, P);
     }
-    if (count) hipLaunchKernelGGL((dev::render_full<true>), grid, block, lds, stream, P);
-    else hipLaunchKernelGGL((dev::render_full<false>), grid, block, lds, stream, P);
+    for (int32_t base = 0; base < P.num_chunks; base += batch) {
+        P.slot_base = base;
+        dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);
+        if (deep) {
+            if (count) hipLaunchKernelGGL((dev::render_full<true, true>), grid, block, lds, stream, P);
+            else hipLaunchKernelGGL((dev::render_full<false, true>), grid, block, lds, stream, P);
+        } else {
+            if (count) hipLaunchKernelGGL((dev::render_full<true, false>), grid, block, lds, stream, P);
+            else hipLaunchKernelGGL((dev::render_full<false, false>), grid, block, lds, stream, P);
+        }
+    }
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
 
 static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {
     if (P.num_chunks == 0) return RT_OK;
-    // dielectrics and area lights: the full trace() (render_full.h); it and spheres/planes
-    // exist only as megakernels
-    const bool full = s->host.has_dielectric || P.num_alights > 0;
+    // dielectrics, area lights and maxRecursionDepth > kMaxDepthGPU: the full trace()
+    // (render_full.h); it and spheres/planes exist only as megakernels
+    const bool full = s->host.has_dielectric || P.num_alights > 0 || P.max_depth > kMaxDepthGPU;
     if (full) return launch_full(r, P, stream, count);
     if (!use_megakernel() && !P.count_ref && !P.has_special) {   // ref-order counting is a megakernel mode
         const bool bounce_w = scene_has_bounce(s->host) && P.max_depth > 0;

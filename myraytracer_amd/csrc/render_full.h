@@ -54,10 +54,27 @@ __device__ __forceinline__ void fresnel_dielectric(double n1, double n2, double 
 
 // EVENTS: count area-light evaluations only (no light sampling, no shadow rays); the
 // paths, PCG32 draws and jitterIndex increments are the same as the real render.
-template <bool COUNT, bool EVENTS>
+// DEEP: maxRecursionDepth > kMaxDepthGPU; levels beyond the private frames live in the
+// launch's deep-frame buffer (RenderParams::deep, one Frame per level and lane of the launch).
+template <bool DEEP>
+struct FrameStack {
+    Frame loc[kMaxDepthGPU + 1];
+    Frame* deep;              // this lane's level kMaxDepthGPU + 1
+    size_t stride;            // lanes of the launch
+    __device__ __forceinline__ Frame& operator[](int d) {
+        if (!DEEP || d <= kMaxDepthGPU) return loc[d];
+        return deep[(size_t)(d - kMaxDepthGPU - 1) * stride];
+    }
+};
+
+template <bool COUNT, bool EVENTS, bool DEEP>
 __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng,
                          long long& jitterIndex, Stack& st, Counts& c) {
-    Frame F[kMaxDepthGPU + 1];
+    FrameStack<DEEP> F;
+    if (DEEP) {
+        F.stride = (size_t)gridDim.x * blockDim.x;
+        F.deep = reinterpret_cast<Frame*>(P.deep) + ((size_t)blockIdx.x * blockDim.x + threadIdx.x);
+    }
     int depth = 0;
     LevelOut out;
     for (;;) {
@@ -244,7 +261,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
 }
 
 // Pixel loop shared by k_events and render_full (Object+Extension.swift:292-356).
-template <bool COUNT, bool EVENTS>
+template <bool COUNT, bool EVENTS, bool DEEP>
 __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, long long& jitterIndex, Stack& st,
                                          Counts& c) {
     const DCamera& C = P.cam;
@@ -277,7 +294,7 @@ __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, lo
             const double time = rng.nextFloat();
             const double denom = dot(dir, w);
             const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
-            pixel = pixel + trace_full<COUNT, EVENTS>(P, camEye, dir, smax(tImg, 0.0), time, rng, jitterIndex, st, c);
+            pixel = pixel + trace_full<COUNT, EVENTS, DEEP>(P, camEye, dir, smax(tImg, 0.0), time, rng, jitterIndex, st, c);
             sampleIndex += 1;
             if (sampleIndex >= C.samples) break;
         }
@@ -291,13 +308,14 @@ __device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int
     const int gx = (P.cam.width + 8 * wpb - 1) / (8 * wpb);
     const int tile = (int)blockIdx.x;
     i = (tile % gx) * (8 * wpb) + wave * 8 + (lane & 7);
-    slot = tile / gx;
+    slot = P.slot_base + tile / gx;
     const int chunk = P.chunk_first + slot * P.chunk_step;
     row = lane >> 3;
     j = chunk * 8 + row;
 }
 
 // Pass 1: area-light evaluations per pixel of the selection (packed rows).
+template <bool DEEP>
 __global__ __launch_bounds__(256) void k_events(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
@@ -306,7 +324,7 @@ __global__ __launch_bounds__(256) void k_events(RenderParams P) {
     Counts cnt{};
     MYRT_STACK(st, lds_stack);
     long long events = 0;
-    (void)pixel_full<false, true>(P, i, j, events, st, cnt);
+    (void)pixel_full<false, true, DEEP>(P, i, j, events, st, cnt);
     P.events[((size_t)slot * 8 + row) * (size_t)P.cam.width + i] = events;
 }
 
@@ -335,7 +353,7 @@ __global__ __launch_bounds__(256) void k_jscan(RenderParams P) {
 }
 
 // Pass 3 (or the only pass without area lights): the render.
-template <bool COUNT>
+template <bool COUNT, bool DEEP>
 __global__ __launch_bounds__(256) void render_full(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
@@ -347,7 +365,7 @@ __global__ __launch_bounds__(256) void render_full(RenderParams P) {
         MYRT_STACK(st, lds_stack);
         const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;   // packed selection index
         long long jitterIndex = P.num_alights > 0 ? P.jstart[q] : 0;
-        const V3 px = pixel_full<COUNT, false>(P, i, j, jitterIndex, st, cnt) / (double)P.cam.samples;
+        const V3 px = pixel_full<COUNT, false, DEEP>(P, i, j, jitterIndex, st, cnt) / (double)P.cam.samples;
         const size_t o = out_row_of(P, j >> 3, row) * (size_t)P.cam.width + i;
         if (P.out_rgb) {
             P.out_rgb[o * 3 + 0] = px.x;

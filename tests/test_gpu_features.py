@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import myraytracer_amd as M
+from myraytracer_amd import _abi as A
 from myraytracer_amd import scenes
 import oracle
 
@@ -189,4 +190,60 @@ def test_scene_file_through_the_engine(tmp_path, fname):
             (ost.primary_rays, ost.shadow_rays, ost.secondary_rays)
     res = eng.save_png(str(tmp_path / "out.png"), 0)
     assert os.path.getsize(tmp_path / "out.png") > 0 and res.file_name == "mixed_lookat.png"
+    eng.close()
+
+
+# ---------------------------------------------------------------- maxRecursionDepth > 16
+def _mirror_corridor(depth, w=64, h=48, glass=False):
+    """A mirror/conductor box corridor (x = +-1, y = +-2) along -z, camera looking mostly
+    sideways: most rays bounce until maxRecursionDepth stops them (trace() :97, :189-206).
+    Levels beyond kMaxDepthGPU = 16 live in the device deep-frame buffer (render_full.h)."""
+    wall = lambda x, m: M.Mesh(id=int(10 + 5 * (x + 1)), material=m,
+                               positions=np.array([[x, -2, 2], [x, 2, 2], [x, 2, -60], [x, -2, -60]], np.float64),
+                               indices=np.array([[1, 2, 3], [1, 3, 4]], np.int32), shading_mode="flat")
+    floor = M.Mesh(id=30, material="2", positions=np.array([[-1, -2, 2], [1, -2, 2], [1, -2, -60], [-1, -2, -60]],
+                                                           np.float64),
+                   indices=np.array([[1, 3, 2], [1, 4, 3]], np.int32), shading_mode="flat")
+    ceiling = M.Mesh(id=31, material="4", positions=np.array([[-1, 2, 2], [1, 2, 2], [1, 2, -60], [-1, 2, -60]],
+                                                             np.float64),
+                     indices=np.array([[1, 2, 3], [1, 3, 4]], np.int32), shading_mode="flat")
+    objs = [wall(-1.0, "2"), wall(1.0, "4"), floor, ceiling]
+    if glass:
+        objs.append(M.Sphere(center=(0.2, -1.2, -6.0), radius=0.6, material="3"))
+    cam = M.Camera(position=(0.0, 0.0, 0.0), gaze_point=(1.0, -0.05, -0.25), up=(0.0, 1.0, 0.0), fovy=40.0,
+                   image_resolution=(w, h))
+    return M.Scene(cameras=[cam], materials=_materials(), objects=objs,
+                   point_lights=[M.PointLight((0.0, 1.5, -4.0), (800.0, 800.0, 800.0))],
+                   ambient_light=(20.0, 20.0, 20.0), background_color=(5.0, 10.0, 20.0),
+                   shadow_ray_epsilon=1e-3, intersection_test_epsilon=1e-6, max_recursion_depth=depth)
+
+
+@pytest.mark.parametrize("depth", [17, 40])
+def test_deep_mirror_recursion(depth):
+    st = _compare(_mirror_corridor(depth))
+    # most primary rays run to the depth limit: far more secondary rays than 16 per pixel allow
+    assert st.secondary_rays > 16 * 64 * 48 // 2
+
+
+def test_deep_recursion_with_glass_and_area_light():
+    sc = _mirror_corridor(24, 48, 36, glass=True)
+    sc.area_lights = [M.AreaLight(position=(0.0, 1.9, -5.0), normal=(0.0, -1.0, 0.0), size=0.8,
+                                  radiance=(60.0, 60.0, 60.0))]
+    _compare(sc)
+
+
+def test_deep_recursion_batched_launches(monkeypatch):
+    """Frames whose deep levels exceed one launch's buffer are rendered in chunk batches
+    (render.hip launch_full): 16 tiles x 64 lanes x 284 levels x 128 B = 37 MB per chunk,
+    so a 40 MB cap gives one chunk per launch.  The result must not depend on the batching."""
+    monkeypatch.setenv("MYRT_DEEP_CAP_MB", "40")
+    _compare(_mirror_corridor(300, 128, 64), chunk_first=1, chunk_step=2)
+
+
+def test_deep_recursion_refused_past_the_buffer(monkeypatch):
+    monkeypatch.setenv("MYRT_DEEP_CAP_MB", "1")
+    eng = M.RayTracerEngine(_mirror_corridor(300, 128, 64))
+    with pytest.raises(M.RenderError) as e:
+        eng.render(0)
+    assert e.value.code == A.RT_ERR_UNSUPPORTED
     eng.close()
