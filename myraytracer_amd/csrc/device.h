@@ -1008,11 +1008,224 @@ __device__ __forceinline__ bool uni_occluded_f32(const RenderParams& P, const V3
     return r == 2;
 }
 
+// ------------------------------------------------------------------ packet walks (MYRT_PACKET)
+// Identity scenes, wave-coherent rays (primary rays of an 8x8 tile, their shadow rays): the
+// whole wave walks ONE node sequence, the union of what its lanes need.  Each step's record
+// or triangle is wave-uniform, so it arrives through the scalar cache (no per-lane vector
+// loads) and the control flow never splits into an inner-node and a leaf branch; a lane
+// takes part in a step when the node is in its mask (its box test hit, within its own
+// pruning limit).
+//   * Stack: {ref, lane mask} entries in the wave's LDS stack slab (the per-lane stack is
+//     empty while a packet walk runs; 512 entries, the host bound is kStackCap).
+//   * Closest hit: at a node where lanes want both children the wave takes the majority's
+//     near child first.  A lane whose own near-first order (RTContext.swift:600-606) differs
+//     is flagged; the order only decides which of two EQUAL-t hits wins (H2; pruned subtrees
+//     cannot hold the final hit, H3), so a flagged lane that also met an equal-t candidate
+//     is walked again alone in the reference order (uni_closest_walk).  Every other lane's
+//     result is the reference's.
+//   * Any hit: order-free; a lane leaves the packet at its first occluder.
+#ifndef MYRT_PACKET
+#define MYRT_PACKET 0      // measured slower (DESIGN §4 lost experiments): compiled out by default
+#endif
+typedef const __attribute__((address_space(4))) WRec c4_wrec;
+typedef const __attribute__((address_space(4))) TriRec c4_tri;
+typedef const __attribute__((address_space(4))) DInstance c4_inst;
+typedef const __attribute__((address_space(4))) DTlasLeafEntry c4_leaf;
+__device__ __forceinline__ int wuni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ unsigned long long wuni64(unsigned long long x) {
+    return (unsigned long long)(unsigned)wuni((int)(unsigned)x) |
+           ((unsigned long long)(unsigned)wuni((int)(unsigned)(x >> 32)) << 32);
+}
+// wave-uniform stack entry k = {ref, mask} at slab[2k], slab[2k + 1]; one lane stores it
+__device__ __forceinline__ void wpush(lds_u64* slab, int& sp, int ref, unsigned long long mask) {
+    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+        slab[2 * sp] = (unsigned long long)(unsigned)ref;
+        slab[2 * sp + 1] = mask;
+    }
+    ++sp;
+}
+__device__ __forceinline__ void wpop(lds_u64* slab, int& sp, int& ref, unsigned long long& mask) {
+    --sp;
+    ref = wuni((int)(unsigned)slab[2 * sp]);
+    mask = wuni64(slab[2 * sp + 1]);
+}
+__device__ __forceinline__ bool lane_in(unsigned long long m) { return (m >> (threadIdx.x & 63)) & 1ull; }
+// wave-uniform records read through the constant address space: scalar (s_load) loads
+__device__ __forceinline__ WRec load_wrec_uniform(const WRec* g) {
+    c4_wrec* p = (c4_wrec*)g;
+    WRec R;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { R.lo[c][k] = p->lo[c][k]; R.hi[c][k] = p->hi[c][k]; }
+        R.ref[c] = p->ref[c];
+    }
+    return R;
+}
+__device__ __forceinline__ TriRec load_tri_uniform(const TriRec* g) {
+    c4_tri* p = (c4_tri*)g;
+    TriRec T;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { T.v0[k] = p->v0[k]; T.e1[k] = p->e1[k]; T.e2[k] = p->e2[k]; }
+    T.last = p->last;
+    T.prim = p->prim;
+    return T;
+}
+
+// Closest hit, every lane's 1/d finite (FAST slabs).  Returns true when this lane must be
+// walked again in the reference order (order deviation + equal-t candidate).
+__device__ __forceinline__ bool uni_closest_packet(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
+                                                   double tlo, Hit& h, Stack& st) {
+    lds_u64* slab = st.lds - (threadIdx.x & 63);
+    double d0;
+    unsigned long long m = __ballot(slab_hit<true>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2],
+                                                   P.tlas_root_hi[0], P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv,
+                                                   P.eps, d0));
+    if (!m) return false;
+    int ref = P.tlas_root_ref, sp = 0;
+    bool dev = false, tie = false;
+    for (;;) {
+        const bool in = lane_in(m);
+        if (ref >= 0) {
+            const WRec R = load_wrec_uniform(P.recs + ref);
+            double t0 = 0, t1 = 0;
+            bool h0 = false, h1 = false;
+            if (in) {
+                const double lim = h.t * P.prune_rel + P.prune_abs;
+                h0 = slab_hit<true>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
+                                    P.eps, t0) && !(t0 > lim);
+                h1 = slab_hit<true>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
+                                    P.eps, t1) && !(t1 > lim);
+            }
+            const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
+            if (m0 && m1) {
+                const bool both = h0 && h1, sw = both && (t0 > t1);
+                const bool wswap = 2 * __popcll(__ballot(sw)) > __popcll(__ballot(both));
+                dev = dev || (both && sw != wswap);
+                wpush(slab, sp, wswap ? R.ref[0] : R.ref[1], wswap ? m0 : m1);
+                ref = wswap ? R.ref[1] : R.ref[0];
+                m = wswap ? m1 : m0;
+                continue;
+            }
+            if (m0 | m1) {
+                ref = m0 ? R.ref[0] : R.ref[1];
+                m = m0 | m1;
+                continue;
+            }
+        } else {
+            const int e = ~ref;
+            if (e < P.tlas_leaf_base) {                          // BLAS leaf run, in leaf order
+                for (int t = e;; ++t) {
+                    const TriRec T = load_tri_uniform(P.tris + t);
+                    if (in) tri_closest_tie(T, o, d, tlo, P.eps, h, t, T.prim, tie);
+                    if (T.last) break;
+                }
+            } else {                                             // TLAS leaf: roots pushed in reverse
+                const int k0 = e - P.tlas_leaf_base;
+                int k1 = k0;
+                while (!((c4_leaf*)P.tlas_leaf)[k1].last) ++k1;
+                for (int k = k1; k >= k0; --k) {
+                    const c4_inst& I = ((c4_inst*)P.insts)[((c4_leaf*)P.tlas_leaf)[k].inst];
+                    double dr;
+                    bool hb = false;
+                    if (in) hb = slab_hit<true>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                                                I.root_hi[2], o, inv, P.eps, dr) &&
+                                 !(dr > h.t * P.prune_rel + P.prune_abs);
+                    const unsigned long long mk = __ballot(hb);
+                    if (mk) wpush(slab, sp, I.root_ref, mk);
+                }
+            }
+        }
+        if (sp == 0) break;
+        wpop(slab, sp, ref, m);
+    }
+    return dev && tie;
+}
+
+// Any hit; `live` = this lane has a shadow ray.  Returns the lane's occlusion.
+__device__ __forceinline__ bool uni_occluded_packet(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
+                                                    double tmax, Stack& st) {
+    lds_u64* slab = st.lds - (threadIdx.x & 63);
+    const double lim = tmax * P.prune_rel + P.prune_abs;
+    double d0;
+    unsigned long long alive = __ballot(slab_hit<true>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2],
+                                                       P.tlas_root_hi[0], P.tlas_root_hi[1], P.tlas_root_hi[2], o,
+                                                       inv, P.eps, d0) && !(d0 > lim));
+    const unsigned long long entered = alive;
+    int ref = P.tlas_root_ref, sp = 0;
+    unsigned long long m = alive;
+    for (;;) {
+        const bool in = lane_in(m);
+        if (ref >= 0) {
+            const WRec R = load_wrec_uniform(P.recs + ref);
+            double t0, t1;
+            bool h0 = false, h1 = false;
+            if (in) {
+                h0 = slab_hit<true>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
+                                    P.eps, t0) && !(t0 > lim);
+                h1 = slab_hit<true>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
+                                    P.eps, t1) && !(t1 > lim);
+            }
+            const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
+            if (m0 && m1) {                                      // L first (any-hit order is free)
+                wpush(slab, sp, R.ref[1], m1);
+                ref = R.ref[0];
+                m = m0;
+                continue;
+            }
+            if (m0 | m1) {
+                ref = m0 ? R.ref[0] : R.ref[1];
+                m = m0 | m1;
+                continue;
+            }
+        } else {
+            const int e = ~ref;
+            if (e < P.tlas_leaf_base) {
+                bool occ = false;
+                for (int t = e;; ++t) {
+                    const TriRec T = load_tri_uniform(P.tris + t);
+                    if (in && !occ) occ = tri_shadow(T, o, d, 0.0, tmax, P.eps);
+                    if (T.last) break;
+                }
+                alive &= ~__ballot(occ);
+                if (!alive) break;
+            } else {
+                const int k0 = e - P.tlas_leaf_base;
+                int k1 = k0;
+                while (!((c4_leaf*)P.tlas_leaf)[k1].last) ++k1;
+                for (int k = k1; k >= k0; --k) {
+                    const c4_inst& I = ((c4_inst*)P.insts)[((c4_leaf*)P.tlas_leaf)[k].inst];
+                    double dr;
+                    bool hb = false;
+                    if (in) hb = slab_hit<true>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
+                                                I.root_hi[2], o, inv, P.eps, dr) && !(dr > lim);
+                    const unsigned long long mk = __ballot(hb);
+                    if (mk) wpush(slab, sp, I.root_ref, mk);
+                }
+            }
+        }
+        for (;;) {                                               // pop an entry with live lanes
+            if (sp == 0) return lane_in(entered & ~alive);
+            wpop(slab, sp, ref, m);
+            m &= alive;
+            if (m) break;
+        }
+    }
+    return lane_in(entered & ~alive);
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
                                             double tlo, Hit& h, Stack& st, Counts& c) {
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     if (__all(finite3(inv))) {
+        if (MYRT_PACKET && !COUNT && (P.packet & 1)) {
+            if (uni_closest_packet(P, o, d, inv, tlo, h, st)) {      // rare: reference order again
+                h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+                uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
+            }
+            return;
+        }
         if (MYRT_F32 && !COUNT && P.use_f32) uni_closest_f32(P, o, d, inv, tlo, h, st, c);
         else uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
     } else {
@@ -1042,6 +1255,7 @@ __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o,
     if (!P.has_tlas) return false;
     const V3 inv = rcp(d);
     if (__all(finite3(inv))) {
+        if (MYRT_PACKET && !COUNT && (P.packet & 2)) return uni_occluded_packet(P, o, d, inv, tmax, st);
         if (MYRT_F32 && !COUNT && P.use_f32) return uni_occluded_f32(P, o, d, inv, tmax, st, c);
         return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
     }

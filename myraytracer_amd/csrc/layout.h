@@ -139,6 +139,7 @@ struct RenderParams {
     int32_t compact_limit;           // records below this index are read from crecs
     int32_t rot_slots;               // megakernel dispatch order: selected chunk rows rotated by this many
     int32_t lds_top_n;               // megakernel: compact records [0, n) served from LDS (0 = off)
+    int32_t packet;                  // identity scenes: wave packet walks (device.h MYRT_PACKET)
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)

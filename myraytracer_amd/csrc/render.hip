@@ -666,6 +666,8 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
         const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0
         P.compact_limit = (ce && ce[0] == '0') ? 0 : (int32_t)S.compact_records;
+        const char* pe = std::getenv("MYRT_PACKET");            // A/B switch: MYRT_PACKET=0
+        P.packet = pe ? std::atoi(pe) : 3;                     // bit 0: closest hit, bit 1: any hit
         const char* te = std::getenv("MYRT_CTRI");              // A/B switch: MYRT_CTRI=0
         P.ctris = (S.compact_tris && !(te && te[0] == '0')) ? r.ctris : nullptr;
         // near-root records in LDS (megakernel; launch() clears it for the other kernels)

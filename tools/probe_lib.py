@@ -37,8 +37,13 @@ if len(sys.argv) > 2 and sys.argv[2] == "--child":
     sys.exit(0)
 cfg = sys.argv[1]
 for rnd in range(2):
-    for lib in sys.argv[2:]:
+    for spec in sys.argv[2:]:
+        # LIB or LIB:VAR=VALUE,... (environment switches read per launch)
+        lib, _, envs = spec.partition(":")
         env = dict(os.environ, MYRT_LIB=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in envs.split(",") if kv)
+        if envs:
+            print(f"  [{envs}]", flush=True)
         r = subprocess.run([sys.executable, os.path.abspath(__file__), cfg, "--child"], env=env)
         if r.returncode != 0:
             sys.exit(r.returncode)
