@@ -262,7 +262,11 @@ __device__ __forceinline__ bool slab_hit(double lx, double ly, double lz, double
     if (FAST) {
         tmin = fmax(fmax(mnx, mny), mnz);
         tmax = fmin(mxx, fmin(mxy, mxz));
-        hit = tmax >= fmax(tmin, eps);
+#ifndef MYRT_HIT2
+#define MYRT_HIT2 1
+#endif
+        // no NaN here, so tmax >= max(tmin, eps) <=> tmax >= tmin && tmax >= eps
+        hit = MYRT_HIT2 ? (tmax >= tmin && tmax >= eps) : (tmax >= fmax(tmin, eps));
     } else {
         tmin = smax(smax(mnx, mny), mnz);
         tmax = smin(mxx, smin(mxy, mxz));
@@ -523,8 +527,12 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
 #ifndef MYRT_SCALAR_FULL
 #define MYRT_SCALAR_FULL 1
 #endif
+#ifndef MYRT_SCALAR_WREC
+#define MYRT_SCALAR_WREC 1      // measured: C3 -0.5 %, C5 -0.5 % with MYRT_HIT2
+#endif
     if (P.scalar_nodes && __all(ref == r0)) {
-        if (r0 < P.compact_limit) {
+        // MYRT_SCALAR_WREC: the wave-uniform step reads the FP64 record (no v_cvt_f64_f32)
+        if (!MYRT_SCALAR_WREC && r0 < P.compact_limit) {
             const SCRec R = load_crec_scalar(P.crecs + r0);
             return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
         }
