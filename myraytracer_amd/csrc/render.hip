@@ -36,9 +36,18 @@ namespace dev {
 // trace() (Object+Extension.swift:96-283) for diffuse/mirror/conductor materials and
 // point lights.  The recursion Lo + M*trace(depth+1) is run forward and combined
 // backward with the same per-level NaN guard, so the result is the recursive one.
+// `rng_slot`: this lane's LDS slot for the PCG32 state (BOUNCE: the state waits there while
+// the rays are traced instead of being live - spilled - across the walks; nullptr = keep it)
 template <bool COUNT, bool BOUNCE, bool UNI>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
-                         Counts& c) {
+                         Counts& c, __attribute__((address_space(3))) double* rng_slot) {
+    auto park = [&]() { if (BOUNCE && rng_slot) *rng_slot = __builtin_bit_cast(double, rng.state); };
+    auto unpark = [&]() {
+        if (BOUNCE && rng_slot) {
+            asm volatile("" ::: "memory");
+            rng.state = __builtin_bit_cast(unsigned long long, (double)*rng_slot);
+        }
+    };
     V3 Lst[BOUNCE ? kMaxDepthGPU : 1], Mst[BOUNCE ? kMaxDepthGPU : 1];
     int depth = 0;
     V3 L;
@@ -46,11 +55,15 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         if (!P.has_tlas) { L = v3(0, 0, 0); break; }
         const V3 inv = rcp(d);
         Hit h;
+        park();
         if (UNI) uni_closest<COUNT>(P, o, d, inv, tlo, h, st, c);
         else intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
+        unpark();
         if (h.inst < 0) { L = ld3(P.background); break; }
         V3 p, Ngeo;
-        hit_geometry<COUNT>(P, o, d, time, h, p, Ngeo, c);
+        // identity scenes do not move (scene.cpp): motion*time == motion*0 for every time in
+        // [0, 1), so `time` need not stay live across the walk
+        hit_geometry<COUNT>(P, o, d, UNI ? 0.0 : time, h, p, Ngeo, c);
         const DInstance& I = P.insts[h.inst];
         const int matIndex = max(0, min(P.num_mats - 1, I.material - 1));
         const DMaterial& M = P.mats[matIndex];
@@ -87,8 +100,10 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 asm volatile("" : "+v"(contrib.x), "+v"(contrib.y), "+v"(contrib.z));
                 if (NdotL > 0 || MYRT_REF(P)) {
                     c.shadow_traced++;
+                    park();
                     const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
                                              : occluded<COUNT>(P, so, wi, dist, time, st, c);
+                    unpark();
                     if (!blocked && NdotL > 0) Lo = Lo + contrib;
                 }
             }
@@ -245,7 +260,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                 // in LDS while the rays are traced, so they are not live - spilled - across the
                 // walks; the memory clobber makes the reloads real loads.
                 if (!BOUNCE) pacc[3 * 64] = __builtin_bit_cast(double, rng.state);
-                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt);
+                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt, pacc + 3 * 64);
                 asm volatile("" ::: "memory");
                 if (!BOUNCE) {
                     rng.state = __builtin_bit_cast(unsigned long long, (double)pacc[3 * 64]);
@@ -257,7 +272,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                     pacc[0] = pacc[0] + col.x; pacc[64] = pacc[64] + col.y; pacc[128] = pacc[128] + col.z;
                 }
 #else
-                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt);
+                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt, nullptr);
                 pixel = pixel + col;
 #endif
                 sampleIndex += 1;
