@@ -174,8 +174,8 @@ def main():
         fb = M.pinned_array((H, W, 4), np.uint8)
         fb[:] = 0
 
-    def frame():
-        return eng.render_into(0, first, step, rgb=None, rgba=fb, frame_layout=True)
+    # one rt_render_ex call per frame, arguments marshalled once (engine.frame_renderer)
+    frame = eng.frame_renderer(0, first, step, rgb=None, rgba=fb, frame_layout=True)
 
     st = None
     for _ in range(args.warmup):
@@ -187,13 +187,15 @@ def main():
     rays_rank = rays_primary + shadow_traced
 
     # ---- timed region: K frames, barrier + sync on both sides
-    kms = []
+    kms, calls = [], []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_begin = time.perf_counter()
     for _ in range(args.steps):
-        kms.append(frame().kernel_ms)
+        s_ = frame()
+        kms.append(s_.kernel_ms)
+        calls.append(s_.milliseconds)
     torch.cuda.synchronize()
     t_elapsed = time.perf_counter() - t_begin
     if world > 1:
@@ -262,6 +264,9 @@ def main():
                      "note": "value counts shadow rays actually traversed; shadow_cast adds the rays the "
                              "reference casts where N.L <= 0 and discards (value_reference_count)",
                      "secondary_per_step": int(st.secondary_rays) if world == 1 else None},
+            "timing": {"call_ms": round(statistics.mean(calls), 4), "kernel_ms": round(kernel_ms, 4),
+                       "what": "per frame: call_ms = wall time inside rt_render_ex (RenderStats.milliseconds), "
+                               "kernel_ms = HIP events around its launch; ms_per_step - call_ms = Python loop"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gather": gather,
@@ -323,6 +328,13 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
                 "distinct records among the wave's lanes at that step"}
     r["simd_efficiency"] = {"closest": round(wc.lane_steps_closest / max(1, 64 * wc.wave_steps_closest), 3),
                             "shadow": round(wc.lane_steps_shadow / max(1, 64 * wc.wave_steps_shadow), 3)}
+    r["iterations"] = {
+        k: {"wave_iters_inner": int(wc.iter_wave_inner[q]), "wave_iters_leaf": int(wc.iter_wave_leaf[q]),
+            "wave_iters_scalar": int(wc.iter_wave_scalar[q]), "lane_inner": int(wc.iter_lane_inner[q]),
+            "lane_leaf": int(wc.iter_lane_leaf[q])}
+        for q, k in enumerate(("closest", "shadow"))}
+    r["iterations"]["what"] = ("walk iterations of the unified walks: wave iterations in which some lane took an inner "
+                               "step / a leaf run / the wave-uniform scalar inner step, and lane iterations of each kind")
     r["lib_sha256_16"] = lib_sha
     return r
 

@@ -248,6 +248,11 @@ typedef struct rt_work_counters {
     /* Vector-memory redundancy of the inner steps that take per-lane loads (the wave's lanes
      * at more than one record): active lanes vs distinct records among them.             */
     int64_t divergent_lane_loads, divergent_distinct_records;
+    /* Per-iteration divergence of the unified walks ([0] closest hit, [1] any hit): wave
+     * iterations in which some lane took an inner step / a leaf run / the wave-uniform
+     * scalar-cache inner step, and lane iterations that took an inner step / a leaf run.  */
+    int64_t iter_wave_inner[2], iter_wave_leaf[2], iter_wave_scalar[2];
+    int64_t iter_lane_inner[2], iter_lane_leaf[2];
 } rt_work_counters;
 int32_t rt_render_device_counted(rt_scene* scene, int32_t device_slot, int32_t camera_index,
                                  int32_t chunk_first, int32_t chunk_step,
@@ -304,6 +309,10 @@ int32_t rt_debug_trace_rays(rt_scene* scene, int32_t slot, int32_t n, const doub
                             double* out_n, int32_t* out_mat);
 int32_t rt_debug_occluded_rays(rt_scene* scene, int32_t slot, int32_t n, const double* o, const double* d,
                                const double* tmax, const double* time, uint8_t* out);
+/* Reciprocals on device 0 (host arrays, n values): out_fast[i] = the traversal's 1/x
+ * (device.h rcp_rn, used when RenderParams::fast_rcp holds), out_div[i] = IEEE 1.0/x.
+ * Equal bit for bit for 2^-700 <= |x| <= 2^1000 (tests/test_gpu_rays.py).  No scene. */
+int32_t rt_debug_rcp(int32_t n, const double* x, double* out_fast, double* out_div);
 /* Per-wave timeline of one megakernel launch (identity scenes without dielectrics or area
  * lights) into device buffer d_out_rgb: out[3*k..3*k+2] = {start, end, tile} of wave k in
  * 100 MHz ticks (s_memrealtime).  *n_waves = waves launched; at most max_waves are copied.

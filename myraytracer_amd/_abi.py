@@ -85,7 +85,10 @@ class rt_work_counters(C.Structure):
                 ("ref_smooth_hits", C.c_int64), ("ref_pixels", C.c_int64),
                 ("lane_steps_closest", C.c_int64), ("wave_steps_closest", C.c_int64),
                 ("lane_steps_shadow", C.c_int64), ("wave_steps_shadow", C.c_int64),
-                ("divergent_lane_loads", C.c_int64), ("divergent_distinct_records", C.c_int64)]
+                ("divergent_lane_loads", C.c_int64), ("divergent_distinct_records", C.c_int64),
+                ("iter_wave_inner", C.c_int64 * 2), ("iter_wave_leaf", C.c_int64 * 2),
+                ("iter_wave_scalar", C.c_int64 * 2), ("iter_lane_inner", C.c_int64 * 2),
+                ("iter_lane_leaf", C.c_int64 * 2)]
 
 
 class rt_ply_mesh(C.Structure):
@@ -121,6 +124,7 @@ EXPORTED_SYMBOLS = [
     "rt_stats_collect", "rt_rows_for_chunks", "rt_render_device_counted", "rt_last_error", "rt_version",
     "rt_ply_load", "rt_ply_free", "rt_debug_bvh_hash", "rt_debug_host_build",
     "rt_debug_trace_rays", "rt_debug_occluded_rays", "rt_host_alloc", "rt_host_free", "rt_debug_wave_times",
+    "rt_debug_rcp",
     "rt_render_ex", "rt_host_register", "rt_host_unregister",
     "rt_scene_file_load", "rt_scene_file_parse", "rt_scene_file_desc", "rt_scene_file_image_name",
     "rt_scene_file_last_error", "rt_scene_file_destroy",
@@ -183,6 +187,8 @@ def bind(lib: C.CDLL) -> C.CDLL:
     lib.rt_debug_wave_times.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                         P(C.c_uint64), C.c_int64, P(C.c_int64)]
     lib.rt_debug_wave_times.restype = C.c_int32
+    lib.rt_debug_rcp.argtypes = [C.c_int32, c_double_p, c_double_p, c_double_p]
+    lib.rt_debug_rcp.restype = C.c_int32
     lib.rt_debug_bvh_hash.argtypes = [C.c_void_p, C.c_int32]
     lib.rt_debug_bvh_hash.restype = C.c_uint64
     lib.rt_debug_host_build.argtypes = [P(rt_scene_desc), P(C.c_uint64), C.c_int32, c_int32_p, P(rt_scene_info)]

@@ -236,6 +236,9 @@ struct Counts {
     unsigned long long it_closest, it_shadow;   // loop iterations of this lane (divergence study)
     unsigned shadow_traced;                     // shadow rays whose any-hit walk ran (<= shadow)
     unsigned long long div_lanes, div_distinct; // per-lane inner steps / of them, first lane of its record
+    // per walk iteration ([0] closest, [1] any-hit): waves whose lanes took an inner step /
+    // a leaf run / the scalar-cache inner step, and lanes that took an inner step / a leaf
+    unsigned long long it_wave_inner[2], it_wave_leaf[2], it_wave_scalar[2], it_lane_inner[2], it_lane_leaf[2];
 };
 constexpr int kMissRef = 0x7fffffff;   // count_ref any-hit: a pushed child whose slab test missed
 
@@ -279,6 +282,47 @@ __device__ __forceinline__ bool finite3(const V3& a) {
     return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
 }
 
+// Near/far planes picked by the direction's sign (MYRT_NEARSEL).  In a FAST walk every 1/d is
+// finite and no slab value is NaN, and a box has lo <= hi, so (lo - o)*i <= (hi - o)*i when
+// i >= 0 and >= when i < 0 (IEEE rounding is monotone): simd.min/max of the two slab values
+// (hitAABB, RTContext.swift:557-565) is the near/far plane's value itself, up to the sign of
+// a zero, which no later comparison sees.  Choosing the planes first replaces the six FP64
+// min/max of a box by selects of the (float or SGPR) bounds.
+//   SEL 0: min/max (slab_hit); 1: per-lane selects; 2: wave-uniform octant `soct` (bit a set
+//   when 1/d_a < 0) - the selects of SGPR-held bounds are then scalar.
+#ifndef MYRT_NEARSEL
+#define MYRT_NEARSEL 0      // measured slower (DESIGN §4 lost experiments)
+#endif
+template <bool FAST, int SEL, class T>
+__device__ __forceinline__ bool slab_hit_sel(T lx, T ly, T lz, T hx, T hy, T hz, const V3& o, const V3& inv,
+                                             double eps, int soct, double& tmin_out) {
+    if (!FAST || SEL == 0)
+        return slab_hit<FAST>((double)lx, (double)ly, (double)lz, (double)hx, (double)hy, (double)hz, o, inv, eps,
+                              tmin_out);
+    bool sx, sy, sz;
+    if (SEL == 1) {
+        sx = inv.x < 0.0; sy = inv.y < 0.0; sz = inv.z < 0.0;
+    } else {
+        sx = (soct & 1) != 0; sy = (soct & 2) != 0; sz = (soct & 4) != 0;
+    }
+    const T nx = sx ? hx : lx, ny = sy ? hy : ly, nz = sz ? hz : lz;
+    const T fx = sx ? lx : hx, fy = sy ? ly : hy, fz = sz ? lz : hz;
+    const double tnx = ((double)nx - o.x) * inv.x, tny = ((double)ny - o.y) * inv.y,
+                 tnz = ((double)nz - o.z) * inv.z;
+    const double tfx = ((double)fx - o.x) * inv.x, tfy = ((double)fy - o.y) * inv.y,
+                 tfz = ((double)fz - o.z) * inv.z;
+    const double tmin = fmax(fmax(tnx, tny), tnz);
+    const double tmax = fmin(tfx, fmin(tfy, tfz));
+    tmin_out = tmin;
+    return tmax >= tmin && tmax >= eps;          // no NaN: = tmax >= max(tmin, eps)
+}
+// The wave's common octant of 1/d (bit a set when 1/d_a < 0), or -1 when its lanes differ.
+__device__ __forceinline__ int wave_octant(const V3& inv) {
+    const int oct = (inv.x < 0.0 ? 1 : 0) | (inv.y < 0.0 ? 2 : 0) | (inv.z < 0.0 ? 4 : 0);
+    const int o0 = __builtin_amdgcn_readfirstlane(oct);
+    return __all(oct == o0) ? o0 : -1;
+}
+
 // Triangle geometry from either record format (layout.h TriRec / CTri).
 __device__ __forceinline__ void tri_geom(const TriRec& T, V3& v0, V3& e1, V3& e2) {
     v0 = ld3(T.v0); e1 = ld3(T.e1); e2 = ld3(T.e2);
@@ -289,17 +333,39 @@ __device__ __forceinline__ void tri_geom(const CTri& T, V3& v0, V3& e1, V3& e2) 
     e2 = v3((double)T.v2[0], (double)T.v2[1], (double)T.v2[2]) - v0;
 }
 
+// 1/x correctly rounded, for x with 2^-700 <= |x| <= 2^1000 (RenderParams::fast_rcp: the host
+// proves every Moeller-Trumbore determinant of the scene lies there, scene.cpp det bound).
+// This is the compiler's IEEE division sequence for 1.0/x without its range steps: in that
+// range v_div_scale leaves both operands unscaled (and clears VCC, so v_div_fmas is a plain
+// FMA), 1.0*r is exact, and v_div_fixup only re-applies the sign the FMA result already has.
+// Bit-identical to 1.0/x there, in 7 instead of 11 instructions.
+__device__ __forceinline__ double rcp_rn(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double rem = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(rem, r, r);
+}
+#ifndef MYRT_FAST_RCP
+#define MYRT_FAST_RCP 1
+#endif
+__device__ __forceinline__ double inv_det(double det, bool frcp) {
+    return (MYRT_FAST_RCP && frcp) ? rcp_rn(det) : 1.0 / det;
+}
+
 // Closest-hit triangle test, intersectTriangle (RTContext.swift:479-510) minus the
 // hit-point/normal writes, which are recomputed once for the final hit (same values).
 template <class Tri>
 __device__ __forceinline__ bool tri_closest(const Tri& T, const V3& o_mb, const V3& d, double tlo, double eps,
-                                           Hit& h, int triIdx, int instIdx) {
+                                           Hit& h, int triIdx, int instIdx, bool frcp = false) {
     V3 v0, e1, e2;
     tri_geom(T, v0, e1, e2);
     const V3 pvec = cross(d, e2);
     const double det = dot(e1, pvec);
     if (fabs(det) < eps) return false;
-    const double invDet = 1.0 / det;
+    const double invDet = inv_det(det, frcp);
     const V3 tvec = o_mb - v0;
     const double u = dot(tvec, pvec) * invDet;
     if (u < 0.0 || u > 1.0) return false;
@@ -314,13 +380,13 @@ __device__ __forceinline__ bool tri_closest(const Tri& T, const V3& o_mb, const 
 // triShadowHit (RTContext.swift:832-848)
 template <class Tri>
 __device__ __forceinline__ bool tri_shadow(const Tri& T, const V3& o_mb, const V3& d, double tlo, double thi,
-                                           double eps) {
+                                           double eps, bool frcp = false) {
     V3 v0, e1, e2;
     tri_geom(T, v0, e1, e2);
     const V3 pvec = cross(d, e2);
     const double det = dot(e1, pvec);
     if (fabs(det) < eps) return false;
-    const double invDet = 1.0 / det;
+    const double invDet = inv_det(det, frcp);
     const V3 tvec = o_mb - v0;
     const double u = dot(tvec, pvec) * invDet;
     if (u < 0.0 || u > 1.0) return false;
@@ -386,13 +452,15 @@ __device__ __forceinline__ bool prim_shadow(int kind, const TriRec& T, const V3&
 // (true), or the caller must pop (false).  Order = near first, ties to L (the reference
 // pushes R then L after `if d1 > d2 swap`, RTContext.swift:600-606); the far child is
 // pushed.  Children beyond `lim` (conservative t-pruning) count as misses.
-template <bool COUNT, bool FAST, bool SHADOW, class Rec>
+template <bool COUNT, bool FAST, bool SHADOW, int SEL = 0, class Rec>
 __device__ __forceinline__ bool inner_step_rec(const RenderParams& P, const Rec& R, int& ref, const V3& o,
-                                               const V3& inv, double lim, Stack& st, Counts& c) {
+                                               const V3& inv, double lim, Stack& st, Counts& c, int soct = -1) {
     if (COUNT) c.recs++;
     double t0, t1;
-    bool h0 = slab_hit<FAST>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv, P.eps, t0);
-    bool h1 = slab_hit<FAST>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv, P.eps, t1);
+    bool h0 = slab_hit_sel<FAST, SEL>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
+                                      P.eps, soct, t0);
+    bool h1 = slab_hit_sel<FAST, SEL>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
+                                      P.eps, soct, t1);
     h0 = h0 && !(t0 > lim);
     h1 = h1 && !(t1 > lim);
     const int a = R.ref[0], b = R.ref[1];
@@ -522,7 +590,10 @@ __device__ __forceinline__ CRec load_crec56(const CRec* p) {
 // through the scalar cache when the whole wave is at this node.
 template <bool COUNT, bool FAST, bool SHADOW>
 __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
-                                           Stack& st, Counts& c) {
+                                           Stack& st, Counts& c, int soct = -1) {
+    // float bounds in VGPRs: per-lane selects cost what the FP64 min/max they replace cost
+    // (v_cndmask_b32 issues in 4 cycles here, tools/valu_rates.hip; C3 0.769 vs 0.733 ms)
+    constexpr int kLaneSel = MYRT_NEARSEL >= 2 ? 1 : 0;
     const int r0 = __builtin_amdgcn_readfirstlane(ref);
 #ifndef MYRT_SCALAR_FULL
 #define MYRT_SCALAR_FULL 1
@@ -531,6 +602,8 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
 #define MYRT_SCALAR_WREC 1      // measured: C3 -0.5 %, C5 -0.5 % with MYRT_HIT2
 #endif
     if (P.scalar_nodes && __all(ref == r0)) {
+        if (COUNT && !P.count_ref)
+            c.it_wave_scalar[SHADOW] += ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) ? 1 : 0;
         // MYRT_SCALAR_WREC: the wave-uniform step reads the FP64 record (no v_cvt_f64_f32)
         if (!MYRT_SCALAR_WREC && r0 < P.compact_limit) {
             const SCRec R = load_crec_scalar(P.crecs + r0);
@@ -538,6 +611,8 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
         }
 #if MYRT_SCALAR_FULL
         const SRec R = load_rec_scalar(P.recs + r0);
+        if (MYRT_NEARSEL && FAST && soct >= 0)      // FP64 bounds in SGPRs: scalar selects
+            return inner_step_rec<COUNT, FAST, SHADOW, 2>(P, R, ref, o, inv, lim, st, c, soct);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
 #endif
     }
@@ -564,13 +639,13 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
         R.lo[1][1] = b.x; R.lo[1][2] = b.y; R.hi[0][0] = b.z; R.hi[0][1] = b.w;
         R.hi[0][2] = e.x; R.hi[1][0] = e.y; R.hi[1][1] = e.z; R.hi[1][2] = e.w;
         R.ref[0] = f.x; R.ref[1] = f.y;
-        return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
+        return inner_step_rec<COUNT, FAST, SHADOW, kLaneSel>(P, R, ref, o, inv, lim, st, c);
     }
     if (ref < P.compact_limit) {
 #if MYRT_CREC56
-        return inner_step_rec<COUNT, FAST, SHADOW>(P, load_crec56(P.crecs + ref), ref, o, inv, lim, st, c);
+        return inner_step_rec<COUNT, FAST, SHADOW, kLaneSel>(P, load_crec56(P.crecs + ref), ref, o, inv, lim, st, c);
 #else
-        return inner_step_rec<COUNT, FAST, SHADOW>(P, P.crecs[ref], ref, o, inv, lim, st, c);
+        return inner_step_rec<COUNT, FAST, SHADOW, kLaneSel>(P, P.crecs[ref], ref, o, inv, lim, st, c);
 #endif
     }
     return inner_step_rec<COUNT, FAST, SHADOW>(P, P.recs[ref], ref, o, inv, lim, st, c);
@@ -601,9 +676,10 @@ __device__ __forceinline__ bool pop_next(const RenderParams& P, Stack& st, int b
 template <bool COUNT, bool FAST, bool SHADOW, class Leaf, class Limit>
 __device__ __forceinline__ bool walk(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st, int base,
                                      Counts& c, Leaf leaf, Limit limit) {
+    const int soct = FAST ? wave_octant(inv) : -1;
     for (;;) {
         if (ref >= 0) {
-            if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, limit(), st, c)) continue;
+            if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, limit(), st, c, soct)) continue;
         } else {
             if (leaf(ref)) return true;
         }
@@ -651,7 +727,7 @@ __device__ void intersect_closest(const RenderParams& P, const V3& o, const V3& 
                         for (int t = ~r;; ++t) {
                             const auto T = tris[t];          // by value: `last` arrives with the vertices
                             if (COUNT) c.tris++;
-                            const bool closer = tri_closest(T, omb, dl, tlo, eps, h, t, inst);
+                            const bool closer = tri_closest(T, omb, dl, tlo, eps, h, t, inst, P.fast_rcp);
                             if (MYRT_REF(P) && closer && I.smooth) c.smooth++;
                             if (T.last) break;
                         }
@@ -709,7 +785,7 @@ __device__ bool occluded(const RenderParams& P, const V3& o, const V3& d, double
                         for (int t = ~r;; ++t) {
                             const auto T = tris[t];          // by value: `last` arrives with the vertices
                             if (COUNT) c.tris++;
-                            if (tri_shadow(T, omb, dl, 0.0, tmax, eps)) return true;
+                            if (tri_shadow(T, omb, dl, 0.0, tmax, eps, P.fast_rcp)) return true;
                             if (T.last) break;
                         }
                         return false;
@@ -753,8 +829,8 @@ __device__ __forceinline__ bool unified_leaf(const RenderParams& P, int ref, Sta
     if (e < P.tlas_leaf_base) {                                  // BLAS leaf run
         auto test = [&](const auto& T, int t) -> bool {
             if (COUNT) c.tris++;
-            if (SHADOW) return tri_shadow(T, o, d, 0.0, tmax, eps);
-            tri_closest(T, o, d, tlo, eps, h, t, T.prim);            // prim = owning instance
+            if (SHADOW) return tri_shadow(T, o, d, 0.0, tmax, eps, P.fast_rcp);
+            tri_closest(T, o, d, tlo, eps, h, t, T.prim, P.fast_rcp);   // prim = owning instance
             return false;
         };
         auto run = [&](const auto* tris) -> bool {
@@ -788,9 +864,19 @@ __device__ __forceinline__ bool unified_leaf(const RenderParams& P, int ref, Sta
 #endif
 template <bool COUNT, bool SHADOW, bool FAST>
 __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Stack& st, const V3& o, const V3& d,
-                                            const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
+                                            const V3& inv, double tlo, double tmax, Hit& h, Counts& c, int soct = -1) {
+    if (COUNT && !P.count_ref) {             // divergence breakdown of this iteration
+        const bool in = ref >= 0;
+        const unsigned long long bi = __ballot(in), bl = __ballot(!in);
+        const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
+        c.it_wave_inner[SHADOW] += (first && bi) ? 1 : 0;
+        c.it_wave_leaf[SHADOW] += (first && bl) ? 1 : 0;
+        c.it_lane_inner[SHADOW] += in ? 1 : 0;
+        c.it_lane_leaf[SHADOW] += in ? 0 : 1;
+    }
     if (ref >= 0) {
-        if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c))
+        if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c,
+                                            soct))
             return 0;
     } else if (MYRT_ONE_TRI && ~ref < P.tlas_leaf_base) {
         // one triangle per iteration: a lane in a 2-triangle leaf continues with the second
@@ -844,6 +930,68 @@ __device__ __forceinline__ int unified_walk_ww(const RenderParams& P, int ref, S
     }
 }
 
+// Postponed-leaf form of the unified walk.  With leaves handled where they are met, a wave
+// ran its leaf block with ~10 of its 64 lanes (C3 closest hit: 4.9M lane leaf runs in 0.47M
+// wave leaf blocks, rt_work_counters iter_*), and that block - one or two Moeller-Trumbore
+// tests with an FP64 division each - costs about as much as two inner steps.  Here a lane
+// that reaches a BLAS leaf run parks it (`pend`) and keeps traversing; the wave runs the
+// leaf block once P.leaf_batch lanes hold a leaf, or when no lane can step (each active lane
+// has parked a leaf and met a second one, or has exhausted its stack).
+// Exactness: a lane holds one leaf at a time, so it still tests its leaves in its visit
+// order (near first, ties to L); only the pruning limit lags (h.t is updated at the leaf
+// block), which visits more nodes - every one of which the reference visits, as it does not
+// prune - so the closest hit, including which of two equal-t hits wins, is the reference's
+// (RTContext.swift:544-610).  Any-hit walks are order-free and stop at the leaf block that
+// finds an occluder.  Returns true when occluded (any hit).
+#ifndef MYRT_PL
+#define MYRT_PL 0          // measured slower (DESIGN §4 lost experiments): compiled out by default
+#endif
+template <bool COUNT, bool SHADOW, bool FAST>
+__device__ __forceinline__ bool unified_walk_pl(const RenderParams& P, int ref, Stack& st, const V3& o, const V3& d,
+                                                const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
+    const int base = st.sp;
+    int pend = 0;           // parked BLAS leaf run (a leaf ref, < 0); 0 = none
+    bool live = true;       // `ref` holds a node still to process
+    bool occ = false;
+    for (;;) {
+        const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+        if (COUNT) {
+            if (SHADOW) c.it_shadow++; else c.it_closest++;
+            const bool in = live && ref >= 0;
+            const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
+            c.it_wave_inner[SHADOW] += (first && __ballot(in)) ? 1 : 0;
+            c.it_lane_inner[SHADOW] += in ? 1 : 0;
+        }
+        if (live) {
+            bool pop = false;
+            if (ref >= 0) {
+                pop = !inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, lim, st, c);
+            } else if (~ref >= P.tlas_leaf_base) {                  // TLAS leaf: push the BLAS roots
+                unified_leaf<COUNT, SHADOW, FAST>(P, ref, st, o, d, inv, tlo, tmax, h, c);
+                pop = true;
+            } else if (pend == 0) {                                  // park the leaf, move on
+                pend = ref;
+                pop = true;
+            }                                                        // else: wait for the leaf block
+            if (pop) live = pop_next<COUNT, SHADOW>(P, st, base, lim, ref, c);
+        }
+        const bool stuck = !live || (ref < 0 && pend != 0 && ~ref < P.tlas_leaf_base);
+        const unsigned long long held = __ballot(pend != 0);
+        if (held && (__popcll(held) >= P.leaf_batch || __ballot(stuck) == __ballot(1))) {
+            if (COUNT) {
+                const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
+                c.it_wave_leaf[SHADOW] += first ? 1 : 0;
+                c.it_lane_leaf[SHADOW] += pend != 0 ? 1 : 0;
+            }
+            if (pend != 0) {
+                occ = unified_leaf<COUNT, SHADOW, FAST>(P, pend, st, o, d, inv, tlo, tmax, h, c);
+                pend = 0;
+            }
+        }
+        if (occ || (!live && pend == 0)) return occ;
+    }
+}
+
 // Root test of the unified walk (the TLAS root is popped and tested first,
 // RTContext.swift:642-646).  Returns false when the ray misses the whole scene.
 __device__ __forceinline__ bool unified_begin(const RenderParams& P, const V3& o, const V3& inv, double lim, int& ref) {
@@ -861,11 +1009,16 @@ __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3
                                                  double tlo, Hit& h, Stack& st, Counts& c) {
     int ref;
     if (!unified_begin(P, o, inv, DINF, ref)) return;   // the stack is empty here (base 0)
+    if (MYRT_PL && !MYRT_REF(P) && P.leaf_batch > 0) {
+        unified_walk_pl<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c);
+        return;
+    }
     if (MYRT_WHILE_WHILE) {
         unified_walk_ww<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c);
         return;
     }
-    do { if (COUNT) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0);
+    const int soct = FAST ? wave_octant(inv) : -1;
+    do { if (COUNT) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c, soct) == 0);
 }
 // ------------------------------------------------------------ FP32-enclosed walks (MYRT_F32)
 // The reference's slab test is FP64 (hitAABB, RTContext.swift:557-565).  A wave64 FP32 op
@@ -1249,10 +1402,13 @@ __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     const int base = st.sp;
     int r;
-    if (MYRT_WHILE_WHILE) {
+    if (MYRT_PL && !MYRT_REF(P) && P.leaf_batch > 0) {
+        r = unified_walk_pl<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c) ? 2 : 1;
+    } else if (MYRT_WHILE_WHILE) {
         r = unified_walk_ww<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c);
     } else {
-        do { if (COUNT) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0);
+        const int soct = FAST ? wave_octant(inv) : -1;
+        do { if (COUNT) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c, soct)) == 0);
     }
     st.reset(base);
     return r == 2;

@@ -140,6 +140,10 @@ struct RenderParams {
     int32_t rot_slots;               // megakernel dispatch order: selected chunk rows rotated by this many
     int32_t lds_top_n;               // megakernel: compact records [0, n) served from LDS (0 = off)
     int32_t packet;                  // identity scenes: wave packet walks (device.h MYRT_PACKET)
+    int32_t fast_rcp;                // every Moeller-Trumbore |det| >= eps lies in [2^-700, 2^1000]
+                                     // (host bound): 1/det by device.h rcp_rn, bit-identical
+    int32_t leaf_batch;              // identity scenes: postponed-leaf walks run the leaf block once this
+                                     // many lanes hold a leaf (device.h unified_walk_pl; 0 = immediate leaves)
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)
@@ -154,11 +158,12 @@ struct RenderParams {
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
     unsigned long long* counters;    // [0] shadow rays cast, [1] secondary rays, [2..12] work counters,
-                                     // [13] shadow rays traversed (kCounterWords)
+                                     // [13] shadow rays traversed, [16..25] per-iteration divergence
+                                     // breakdown (rt_work_counters; kCounterWords)
     unsigned long long* wave_times;  // debug (rt_debug_wave_times): per wave {start, end, tile} in 100 MHz ticks
 };
 
-constexpr int kCounterWords = 16;   // u64 words behind RenderParams::counters
+constexpr int kCounterWords = 32;   // u64 words behind RenderParams::counters
 constexpr int kCounterShadowTraced = 13;
 constexpr int kMaxDepthGPU = 16;     // trace() levels kept in private memory per lane (deeper: RenderParams::deep)
 constexpr int64_t kDeepBytesCap = 8ll << 30;   // device bytes of deep frames per launch batch
@@ -171,5 +176,9 @@ constexpr int kStackCap = 128;
 // Breadth-first record prefix of the first BLAS that the render kernels copy into LDS at
 // wave start (device.h Stack::top): the near-root levels every ray walks.
 constexpr int kLdsTopMax = 127;
+
+// Postponed-leaf walks (device.h unified_walk_pl): lanes holding a leaf before the wave runs
+// its leaf block (RenderParams::leaf_batch; host switch MYRT_LEAF_BATCH).
+constexpr int kLeafBatchDefault = 0;    // MYRT_PL builds only; measured slower at every batch size
 
 }  // namespace myrt

@@ -335,6 +335,16 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
         if (lane == 0 && !P.count_ref && dl) {
             atomicAdd(&P.counters[14], dl); atomicAdd(&P.counters[15], dd2);
         }
+        for (int k = 0; k < 2; ++k) {
+            const unsigned long long v0 = wave_sum(cnt.it_wave_inner[k]), v1 = wave_sum(cnt.it_wave_leaf[k]),
+                                     v2 = wave_sum(cnt.it_wave_scalar[k]), v3 = wave_sum(cnt.it_lane_inner[k]),
+                                     v4 = wave_sum(cnt.it_lane_leaf[k]);
+            if (lane == 0 && !P.count_ref) {
+                atomicAdd(&P.counters[16 + 5 * k], v0); atomicAdd(&P.counters[17 + 5 * k], v1);
+                atomicAdd(&P.counters[18 + 5 * k], v2); atomicAdd(&P.counters[19 + 5 * k], v3);
+                atomicAdd(&P.counters[20 + 5 * k], v4);
+            }
+        }
     }
 }
 
@@ -426,6 +436,11 @@ struct DeviceReplica {
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;        // rt_render: D2H of finished batches
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // rt_render: the frame's ray counters come back with one async copy into pinned memory
+    // (ready = counters_ready) and are zeroed behind it, off the next frame's critical path
+    unsigned long long* host_counters = nullptr;
+    hipEvent_t counters_ready = nullptr;
+    bool counters_zero = false;               // r.counters hold zeros (rt_render's trailing memset)
     // rt_render staging (grown on demand, reused across calls)
     double* out_d = nullptr; uint8_t* out8_d = nullptr; int64_t out_cap_px = 0;
     double* host_rgb = nullptr; uint8_t* host_rgba = nullptr; int64_t host_cap_px = 0;   // pinned
@@ -461,6 +476,8 @@ static void free_replica(DeviceReplica& r) {
     (void)hipFree(r.deep);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
+    if (r.counters_ready) (void)hipEventDestroy(r.counters_ready);
+    if (r.host_counters) (void)hipHostFree(r.host_counters);
     if (r.stream) (void)hipStreamDestroy(r.stream);
     if (r.copy_stream) (void)hipStreamDestroy(r.copy_stream);
     (void)hipFree(r.out_d); (void)hipFree(r.out8_d);
@@ -517,6 +534,8 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
     }
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
+    HIP_TRY(hipEventCreateWithFlags(&r.counters_ready, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void**)&r.host_counters, kCounterWords * sizeof(unsigned long long), hipHostMallocDefault));
     return RT_OK;
 }
 
@@ -620,6 +639,13 @@ static double prune_abs_for(const HostScene& S, double origin_dist) {
     const double a = std::max(1e-9 * S.scene_extent, mt);
     return std::isfinite(a) ? a : HUGE_VAL;                          // eps <= 0: no pruning
 }
+// RenderParams::fast_rcp: every determinant the triangle tests divide by satisfies
+// 2^-700 <= eps <= |det| <= det_scale * |d| <= 2^1000 for directions with |d| <= dmax
+// (device.h rcp_rn is then bit-identical to 1.0/det).
+static int32_t fast_rcp_for(const HostScene& S, double dmax) {
+    return (S.eps >= 0x1p-700 && std::isfinite(S.det_scale) && std::isfinite(dmax) &&
+            S.det_scale * dmax <= 0x1p1000) ? 1 : 0;
+}
 static double dist_to_center(const HostScene& S, const double p[3]) {
     double d = 0.0;
     for (int k = 0; k < 3; ++k) d += (p[k] - S.scene_center[k]) * (p[k] - S.scene_center[k]);
@@ -651,6 +677,7 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         const double ce[3] = {cam0.position.x, cam0.position.y, cam0.position.z};
         P.prune_abs = prune_abs_for(S, dist_to_center(S, ce) + std::fabs(cam0.aperture_size));
     }
+    P.fast_rcp = fast_rcp_for(S, 2.0);   // rendered directions are normalized (|d| <= 1 + 2^-50)
     {   // FP32-enclosed slabs (slab32.h): eps rounded out, and a bound on every coordinate of an
         // identity scene (every box of the unified walk lies inside the TLAS root box)
         P.eps_up32 = f32slab::up(P.eps);
@@ -683,6 +710,9 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         P.compact_limit = (ce && ce[0] == '0') ? 0 : (int32_t)S.compact_records;
         const char* pe = std::getenv("MYRT_PACKET");            // A/B switch: MYRT_PACKET=0
         P.packet = pe ? std::atoi(pe) : 3;                     // bit 0: closest hit, bit 1: any hit
+        // postponed leaves (device.h unified_walk_pl): the leaf block runs once this many lanes
+        // of the wave hold a leaf, or no lane can step; 0 = each leaf at once (A/B switch)
+        P.leaf_batch = env_int("MYRT_LEAF_BATCH", kLeafBatchDefault, 0, 64);
         const char* te = std::getenv("MYRT_CTRI");              // A/B switch: MYRT_CTRI=0
         P.ctris = (S.compact_tris && !(te && te[0] == '0')) ? r.ctris : nullptr;
         // near-root records in LDS (megakernel; launch() clears it for the other kernels)
@@ -901,6 +931,7 @@ int32_t rt_render_device(rt_scene* s, int32_t slot, int32_t cam, int32_t first, 
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
     HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
+    r.counters_zero = false;
     RenderParams P = make_params(s, r, cam, first, step, d_rgb, d_rgba8);
     return launch(s, r, P, st, false);
 }
@@ -929,6 +960,7 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
     HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
+    r.counters_zero = false;
     RenderParams P = make_params(s, r, cam, first, step, d_rgb, nullptr);
     rc = launch(s, r, P, st, true);                  // 1) work this path executes
     if (rc != RT_OK) return rc;
@@ -936,6 +968,7 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
     unsigned long long c[kCounterWords];
     HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
+    r.counters_zero = false;
     P.count_ref = 1;                                 // 2) the reference's work
     rc = launch(s, r, P, st, true);
     if (rc != RT_OK) return rc;
@@ -950,6 +983,11 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
         out->lane_steps_closest = (int64_t)c[9]; out->wave_steps_closest = (int64_t)c[10];
         out->lane_steps_shadow = (int64_t)c[11]; out->wave_steps_shadow = (int64_t)c[12];
         out->divergent_lane_loads = (int64_t)c[14]; out->divergent_distinct_records = (int64_t)c[15];
+        for (int k = 0; k < 2; ++k) {
+            out->iter_wave_inner[k] = (int64_t)c[16 + 5 * k]; out->iter_wave_leaf[k] = (int64_t)c[17 + 5 * k];
+            out->iter_wave_scalar[k] = (int64_t)c[18 + 5 * k]; out->iter_lane_inner[k] = (int64_t)c[19 + 5 * k];
+            out->iter_lane_leaf[k] = (int64_t)c[20 + 5 * k];
+        }
     }
     return RT_OK;
 }
@@ -1079,7 +1117,9 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
             HIP_TRY(hipHostMalloc((void**)&r.host_rgba, px * 4, hipHostMallocDefault));
             r.host_cap_px = px;
         }
-        HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
+        if (!r.counters_zero)
+            HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
+        r.counters_zero = false;
         HIP_TRY(hipEventRecord(r.ev0, r.stream));
     }
     // batch b of every replica is enqueued before batch b-1 is drained: one batch renders
@@ -1112,6 +1152,16 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
             const int32_t lrc = launch(s, r, P, r.stream, false);
             if (lrc != RT_OK) return lrc;
             HIP_TRY(hipEventRecord(r.batch_done[b], r.stream));
+            if (b == pl.nb - 1) {
+                // last launch of this replica: kernel time ends here; its counters follow
+                // in one async copy and are zeroed behind it (the next frame skips its memset)
+                HIP_TRY(hipEventRecord(r.ev1, r.stream));
+                HIP_TRY(hipMemcpyAsync(r.host_counters, r.counters, kCounterWords * sizeof(unsigned long long),
+                                       hipMemcpyDeviceToHost, r.stream));
+                HIP_TRY(hipEventRecord(r.counters_ready, r.stream));
+                HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
+                r.counters_zero = true;
+            }
             const size_t nrows = (size_t)(pl.batchRow[b + 1] - pl.batchRow[b]);
             if (zerocopy) {                                  // rows already in the caller's buffer
                 HIP_TRY(hipEventRecord(r.batch_copied[b], r.stream));
@@ -1214,20 +1264,20 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
             if (progress && !progress(user, rowsDone, rowsTotal)) cancelled = true;
         }
     }
-    for (int32_t k = 0; k < D; ++k) {
-        if (plan[k].nb == 0) continue;
-        HIP_TRY(hipSetDevice(s->devs[k].device));
-        HIP_TRY(hipEventRecord(s->devs[k].ev1, s->devs[k].stream));
-    }
     double km = 0;
     int64_t sh = 0, se = 0, st = 0;
     for (int32_t k = 0; k < D; ++k) {
         if (plan[k].nb == 0) continue;
         DeviceReplica& r = s->devs[k];
         HIP_TRY(hipSetDevice(r.device));
-        HIP_TRY(hipStreamSynchronize(r.stream));
-        unsigned long long c[kCounterWords];
-        HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
+        if (enqueued < plan[k].nb) {            // cancelled before the last batch: drain, count
+            HIP_TRY(hipEventRecord(r.ev1, r.stream));
+            HIP_TRY(hipMemcpyAsync(r.host_counters, r.counters, kCounterWords * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, r.stream));
+            HIP_TRY(hipEventRecord(r.counters_ready, r.stream));
+        }
+        HIP_TRY(hipEventSynchronize(r.counters_ready));
+        const unsigned long long* c = r.host_counters;
         sh += (int64_t)c[0]; se += (int64_t)c[1]; st += (int64_t)c[kCounterShadowTraced];
         float ms = 0; (void)hipEventElapsedTime(&ms, r.ev0, r.ev1);
         km = std::max(km, (double)ms);
@@ -1344,8 +1394,15 @@ static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o,
     RenderParams P = make_params(s, r, 0, 0, 1, nullptr, nullptr);
     {   // margin for these rays' own origins
         double od = 0.0;
-        for (int32_t k = 0; k < n; ++k) od = std::max(od, dist_to_center(s->host, o + 3 * (size_t)k));
+        double dm = 0.0;
+        for (int32_t k = 0; k < n; ++k) {
+            od = std::max(od, dist_to_center(s->host, o + 3 * (size_t)k));
+            const double* dk = d + 3 * (size_t)k;
+            const double dn = std::sqrt(dk[0] * dk[0] + dk[1] * dk[1] + dk[2] * dk[2]);
+            dm = std::isfinite(dn) ? std::max(dm, dn) : HUGE_VAL;
+        }
         P.prune_abs = prune_abs_for(s->host, od);
+        P.fast_rcp = fast_rcp_for(s->host, 2.0 * dm + 1.0);
     }
     dev::RayBatch B{};
     B.n = n;
@@ -1431,11 +1488,46 @@ int32_t rt_debug_wave_times(rt_scene* s, int32_t slot, int32_t cam, int32_t firs
     HIP_TRY(hipMemsetAsync(r.wave_times, 0, (size_t)waves * 3 * sizeof(unsigned long long), r.stream));
     P.wave_times = r.wave_times;
     HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
+    r.counters_zero = false;
     if ((rc = launch(s, r, P, r.stream, false)) != RT_OK) return rc;
     HIP_TRY(hipStreamSynchronize(r.stream));
     const int64_t n = std::min<int64_t>(waves, max_waves);
     if (out && n > 0) HIP_TRY(hipMemcpy(out, r.wave_times, (size_t)n * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     if (n_waves) *n_waves = waves;
+    return RT_OK;
+}
+
+namespace myrt {
+namespace dev {
+__global__ void k_rcp(int32_t n, const double* x, double* f, double* q) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    f[i] = rcp_rn(x[i]);
+    q[i] = 1.0 / x[i];
+}
+}  // namespace dev
+}  // namespace myrt
+
+int32_t rt_debug_rcp(int32_t n, const double* x, double* out_fast, double* out_div) {
+    if (n < 0 || (n > 0 && (!x || !out_fast || !out_div))) return fail(RT_ERR_INVALID_ARG, "bad arrays");
+    if (n == 0) return RT_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        return fail(RT_ERR_DEVICE, "no HIP device");
+    }
+    HIP_TRY(hipSetDevice(0));
+    double* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, (size_t)n * 3 * sizeof(double)));
+    hipError_t e = hipMemcpy(d, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(dev::k_rcp, dim3((n + 255) / 256), dim3(256), 0, 0, n, d, d + n, d + 2 * (size_t)n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out_fast, d + n, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_div, d + 2 * (size_t)n, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RT_ERR_DEVICE, hipGetErrorString(e));
     return RT_OK;
 }
 

@@ -941,6 +941,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             S.scene_center[0] = S.scene_center[1] = S.scene_center[2] = 0.0;
         S.prune_k = (S.eps > 0) ? 8.0 * std::ldexp(1.0, -53) * pruneK / S.eps : kInf;
         S.max_motion = maxMotion;
+        S.det_scale = pruneK;
     }
     // Identity mode: every instance's transforms are exactly the identity and nothing moves,
     // so the world ray IS the local ray (up to the sign of zeros, which no comparison sees)

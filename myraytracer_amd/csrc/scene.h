@@ -74,6 +74,8 @@ struct HostScene {
     double scene_center[3] = {0, 0, 0};    // world bounds center
     double prune_k = 0.0;                  // MT t-error constant (scene.cpp, "pruning margin")
     double max_motion = 0.0;               // largest instance + triangle motion-blur offset
+    double det_scale = 0.0;                // >= |e1||e2| * ||A||_F over triangle instances: every
+                                           // Moeller-Trumbore |det| <= det_scale * |d_world|
     // ---- bookkeeping / debug
     int64_t n_meshes = 0, n_tris = 0, n_spheres = 0, n_planes = 0;
     std::vector<uint64_t> inst_bvh_hash;   // per instance: canonical hash of its BLAS

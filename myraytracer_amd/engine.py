@@ -240,6 +240,33 @@ class RayTracerEngine:
                                 A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0, C.byref(st), cb, None))
         return _stats(st)
 
+    def frame_renderer(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
+                       rgb: Optional[np.ndarray] = None, rgba: Optional[np.ndarray] = None,
+                       frame_layout: bool = False) -> Callable[[], A.rt_stats]:
+        """render_into with the arguments checked and marshalled once: returns a callable that
+        renders one frame into the same arrays (one rt_render_ex call, no progress callback)
+        and returns the raw rt_stats.  For frame loops whose per-call Python cost should not
+        count as render time (bench.py)."""
+        self.render_into(camera_index, chunk_first, chunk_step, rgb, rgba, frame_layout)   # validates
+        lib = load_library()
+        fn = lib.rt_render_ex
+        h = self._h
+        prgb = rgb.ctypes.data_as(A.c_double_p) if rgb is not None else None
+        prgba = rgba.ctypes.data_as(C.POINTER(C.c_uint8)) if rgba is not None else None
+        flags = A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0
+        st = A.rt_stats()
+        pst = C.byref(st)
+        cb = A.RT_PROGRESS_FN()
+        keep = (rgb, rgba)
+
+        def one() -> A.rt_stats:
+            rc = fn(h, camera_index, chunk_first, chunk_step, prgb, prgba, flags, pst, cb, None)
+            if rc != A.RT_OK:
+                _check(rc)
+            assert keep is not None
+            return st
+        return one
+
     def render(self, camera_index: int = 0, progress: Optional[Callable[[RenderProgress], bool]] = None) -> RenderResult:
         """RayTracerEngine.render(format:cameraIndex:progress:) (RayTracer.swift:115-131)."""
         rgb, rgba, stats = self.render_rows(camera_index, 0, 1, True, progress)

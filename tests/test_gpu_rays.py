@@ -181,3 +181,28 @@ def test_near_degenerate_grazing_hits_and_the_pruning_margin(walk, monkeypatch):
     t, *_ = oracle.OracleScene(sc).trace_rays(O, D)
     tmax = np.where(np.isfinite(t), t * (1 + rng.choice([-1e-12, 1e-12], size=len(t))), 1e3)
     _check_occluded(sc, O, D, tmax)
+
+
+def test_fast_reciprocal_is_ieee_division():
+    """device.h rcp_rn (1/det of the triangle tests when RenderParams::fast_rcp holds) equals
+    IEEE 1.0/x bit for bit over its range 2^-700 <= |x| <= 2^1000: random mantissas at every
+    exponent, both signs, powers of two, all-ones mantissas and the range ends."""
+    import ctypes as C
+    lib = M.load_library()
+    rng = np.random.RandomState(7)
+    exps = np.arange(-700, 1001)
+    xs = [np.ldexp(1.0 + rng.random_sample(exps.size), exps),           # random mantissas
+          np.ldexp(np.ones(exps.size), exps),                            # powers of two
+          np.ldexp(np.full(exps.size, 2.0 - 2.0 ** -52), exps),          # all-ones mantissas
+          np.ldexp(1.0 + 2.0 ** -52 * np.arange(1, exps.size + 1), exps),
+          rng.uniform(1e-9, 1e9, 200000),                                 # determinants seen in scenes
+          np.array([2.0 ** -700, 2.0 ** 1000, 3.0, 1.0 / 3.0, 0.1, 1e-7, 7e-300, 6e299])]
+    x = np.concatenate(xs)
+    x = np.concatenate([x, -x]).astype(np.float64)
+    fast = np.empty_like(x)
+    div = np.empty_like(x)
+    p = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    assert lib.rt_debug_rcp(int(x.size), p(x), p(fast), p(div)) == 0
+    assert np.array_equal(div.view(np.uint64), (1.0 / x).view(np.uint64))   # the GPU division is IEEE
+    bad = np.flatnonzero(fast.view(np.uint64) != div.view(np.uint64))
+    assert bad.size == 0, (x[bad[:5]], fast[bad[:5]], div[bad[:5]])
