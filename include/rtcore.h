@@ -315,7 +315,8 @@ int32_t rt_debug_occluded_rays(rt_scene* scene, int32_t slot, int32_t n, const d
 int32_t rt_debug_rcp(int32_t n, const double* x, double* out_fast, double* out_div);
 /* Per-wave timeline of one megakernel launch (identity scenes without dielectrics or area
  * lights) into device buffer d_out_rgb: out[3*k..3*k+2] = {start, end, tile} of wave k in
- * 100 MHz ticks (s_memrealtime).  *n_waves = waves launched; at most max_waves are copied.
+ * 100 MHz ticks (s_memrealtime); the tile word also holds the wave's largest lane iteration
+ * counts of the closest-hit walks (bits 24-43) and the any-hit walks (bits 44-63).  *n_waves = waves launched; at most max_waves are copied.
  * Returns RT_ERR_UNSUPPORTED unless the library was built with -DMYRT_WAVE_TIMES=1. */
 int32_t rt_debug_wave_times(rt_scene* scene, int32_t slot, int32_t camera_index, int32_t chunk_first,
                             int32_t chunk_step, double* d_out_rgb, uint64_t* out, int64_t max_waves,

@@ -244,6 +244,9 @@ constexpr int kMissRef = 0x7fffffff;   // count_ref any-hit: a pushed child whos
 
 // reference-order counting requested (a runtime flag read only by COUNT instantiations)
 #define MYRT_REF(P) (COUNT && (P).count_ref)
+#ifndef MYRT_WAVE_TIMES
+#define MYRT_WAVE_TIMES 0    // per-wave timeline for rt_debug_wave_times (debug builds only: costs SGPRs)
+#endif
 
 struct Hit { double t, u, v; int tri, inst; };
 
@@ -1018,7 +1021,7 @@ __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3
         return;
     }
     const int soct = FAST ? wave_octant(inv) : -1;
-    do { if (COUNT) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c, soct) == 0);
+    do { if (COUNT || MYRT_WAVE_TIMES) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c, soct) == 0);
 }
 // ------------------------------------------------------------ FP32-enclosed walks (MYRT_F32)
 // The reference's slab test is FP64 (hitAABB, RTContext.swift:557-565).  A wave64 FP32 op
@@ -1408,7 +1411,7 @@ __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V
         r = unified_walk_ww<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c);
     } else {
         const int soct = FAST ? wave_octant(inv) : -1;
-        do { if (COUNT) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c, soct)) == 0);
+        do { if (COUNT || MYRT_WAVE_TIMES) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c, soct)) == 0);
     }
     st.reset(base);
     return r == 2;

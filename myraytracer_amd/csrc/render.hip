@@ -148,9 +148,6 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 
 
 // One wave renders an 8x8 tile of one 8-row chunk; blocks hold block_threads()/64 waves.
-#ifndef MYRT_WAVE_TIMES
-#define MYRT_WAVE_TIMES 0    // per-wave timeline for rt_debug_wave_times (debug builds only: costs SGPRs)
-#endif
 #ifndef MYRT_MEGA_WPE
 #define MYRT_MEGA_WPE 4      // amdgpu_waves_per_eu for the megakernel (0 = compiler default = 2 waves at ~200 VGPRs)
 #endif
@@ -301,9 +298,12 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 #if MYRT_WAVE_TIMES
     if (P.wave_times) {                                              // debug timeline
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        // the wave's walk iterations: its longest lane's, closest hit and any hit
+        const unsigned long long mc = wave_max(cnt.it_closest), ms = wave_max(cnt.it_shadow);
         if (lane == 0) {
             unsigned long long* w = P.wave_times + 3 * ((size_t)blockIdx.x * wpb + wave);
-            w[0] = t_start; w[1] = t_end; w[2] = (unsigned long long)tile;
+            w[0] = t_start; w[1] = t_end;
+            w[2] = (unsigned long long)tile | (std::min(mc, 0xFFFFFull) << 24) | (std::min(ms, 0xFFFFFull) << 44);
         }
     }
 #endif
