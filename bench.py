@@ -6,13 +6,17 @@ Workload (BASELINE.json configs[2], "C3"): a ~1.02M-triangle single-mesh PLY sce
 1920x1080, 1 spp, 1 point light, shadow rays on, FP64 throughout.
 
 One "step" = one frame through the public render path, timed as SURVEY.md §8(d) defines
-it: `rt_render` wall time with the scene resident in HBM, INCLUDING the device->host
-delivery of the image and the host gather.  The image is what the reference's public
+it: render wall time with the scene resident in HBM, INCLUDING the device->host delivery
+of the image and the host gather.  The image is what the reference's public
 `RayTracerEngine.render` returns - RGBA8 (RayTracer.swift:115-131, 166-203: its render
 time spans Renderer.render + the RGBA8 conversion).  The kernels store the RGBA8 rows
-straight into a page-locked host framebuffer (host-mapped, over PCIe).  Side fields time
-the FP64 [Vec3] framebuffer delivered the same way (`fp64_path`) and the device-only
-launch (`device_only`).
+straight into a page-locked host framebuffer (host-mapped, over PCIe).  The reference's
+render is `async`; frames go through rt_render_submit / rt_render_wait with `--in-flight`
+(default 4) renders in flight, frame k into framebuffer k mod Q, so the next frame's tiles
+fill the compute units the previous frame's slowest tiles leave idle; value = K frames
+delivered / wall time.  `timing.submit_to_done_ms` is one frame's latency.  Side fields
+time the FP64 [Vec3] framebuffer delivered synchronously (`fp64_path`, rt_render) and the
+device-only launch (`device_only`).
 
 N GPUs: one process per GPU (torchrun; `python bench.py --gpus N` starts torchrun itself
 before anything touches a GPU).  Default for N>1 is configs[3] "C4", STRONG scaling: ONE
@@ -40,6 +44,7 @@ infrastructure), rank 0, N = 1: median over whole frames at the box's CPU share,
 from __future__ import annotations
 
 import argparse
+import collections
 import hashlib
 import json
 import mmap
@@ -64,6 +69,8 @@ def parse():
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong (default): one frame per step split over the ranks (C4); "
                         "weak: every rank renders a full frame per step")
+    p.add_argument("--in-flight", type=int, default=4,
+                   help="renders in flight (rt_render_submit); 1 = one synchronous frame at a time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-side-paths", action="store_true", help="skip the fp64 / device-only side measurements")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share (OMP_NUM_THREADS / affinity)")
@@ -140,6 +147,7 @@ def main():
     torch.cuda.set_device(local)
 
     import myraytracer_amd as M
+    from myraytracer_amd import _abi as A
     from myraytracer_amd import scenes
 
     t0 = time.time()
@@ -164,40 +172,56 @@ def main():
     rows = M.rows_for_chunks(H, first, step)
     n = int(max(1, cam.num_samples) ** 0.5)
 
-    # ---- the framebuffer the image is delivered into (RGBA8, whole frame, row 0 = top)
+    # ---- the framebuffers the images are delivered into (RGBA8, whole frame, row 0 = top): one
+    # per render in flight; frame k goes to framebuffer k mod Q
+    Q = max(1, min(args.in_flight, A.RT_MAX_IN_FLIGHT))
+    shared = []
     if strong and world > 1:
-        shared = SharedFrame(W * H * 4, rank, world, dist, args.config)
-        M.register_host(shared.array)
-        fb = shared.array.reshape(H, W, 4)
+        for q in range(Q):
+            sf = SharedFrame(W * H * 4, rank, world, dist, f"{args.config}{q}")
+            M.register_host(sf.array)
+            shared.append(sf)
+        fbs = [sf.array.reshape(H, W, 4) for sf in shared]
     else:
-        shared = None
-        fb = M.pinned_array((H, W, 4), np.uint8)
-        fb[:] = 0
+        fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
+        for fb_ in fbs:
+            fb_[:] = 0
 
-    # one rt_render_ex call per frame, arguments marshalled once (engine.frame_renderer)
-    frame = eng.frame_renderer(0, first, step, rgb=None, rgba=fb, frame_layout=True)
+    # frames through rt_render_submit / rt_render_wait with Q renders in flight (the reference's
+    # render is async, RayTracer.swift:137-205), arguments marshalled once (engine.frame_pipeline)
+    submit, wait = eng.frame_pipeline(0, first, step, fbs, frame_layout=True)
 
-    st = None
-    for _ in range(args.warmup):
-        st = frame()
-    if st is None:
-        st = frame()
+    def run(k_frames, stats_out=None):
+        pend = collections.deque()
+        for k in range(k_frames):
+            if len(pend) == Q:
+                s_ = wait(pend.popleft())
+                if stats_out is not None:
+                    stats_out.append((s_.kernel_ms, s_.milliseconds))
+            pend.append(submit(k))
+        last = None
+        while pend:
+            last = wait(pend.popleft())
+            if stats_out is not None:
+                stats_out.append((last.kernel_ms, last.milliseconds))
+        return last
+
+    st = run(max(1, args.warmup))
     rays_primary = rows * W * n * n
     shadow_cast, shadow_traced = int(st.shadow_rays), int(st.shadow_rays_traced)
     rays_rank = rays_primary + shadow_traced
 
     # ---- timed region: K frames, barrier + sync on both sides
-    kms, calls = [], []
+    per = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_begin = time.perf_counter()
-    for _ in range(args.steps):
-        s_ = frame()
-        kms.append(s_.kernel_ms)
-        calls.append(s_.milliseconds)
+    run(args.steps, per)
     torch.cuda.synchronize()
     t_elapsed = time.perf_counter() - t_begin
+    kms = [a for a, _ in per]
+    calls = [b for _, b in per]
     if world > 1:
         dist.barrier()
     kernel_ms = statistics.mean(kms)
@@ -223,8 +247,10 @@ def main():
         dist.barrier()
     gather = None
     if rank == 0:
-        gather = {"rows_complete": bool(np.all(fb[:, :, 3] == 255)),
-                  "rgba8_sha256": hashlib.sha256(np.ascontiguousarray(fb).tobytes()).hexdigest()}
+        fb = fbs[(args.steps - 1) % Q]                       # the last frame delivered
+        gather = {"rows_complete": bool(all(np.all(f_[:, :, 3] == 255) for f_ in fbs)),
+                  "rgba8_sha256": hashlib.sha256(np.ascontiguousarray(fb).tobytes()).hexdigest(),
+                  "frames_identical": bool(all(np.array_equal(f_, fb) for f_ in fbs))}
 
     # ---- roofline (profiles/roofline_<config>.json: PMC passes of this build, tools/pmc_roofline.py)
     roofline = roofline_fields(args, eng, local, first, step, rows, W, kernel_ms, rays_rank, world)
@@ -242,8 +268,8 @@ def main():
             log("cpu baseline failed:", e)
             cpu = {"value": None, "unit": "Mrays/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 
-    if shared is not None:
-        shared.close(dist)
+    for sf in shared:
+        sf.close(dist)
     if rank == 0:
         line = {
             "metric": "Mrays/s (primary+shadow), 1920x1080 / 1M-tri PLY, at 1/2/4/8 MI355X",
@@ -254,9 +280,10 @@ def main():
             "config": {"workload": workload, "width": W, "height": H, "spp": max(1, cam.num_samples),
                        "triangles": int(info.triangles),
                        "partition": (f"one frame per step, 8-row chunks round-robin over {world} GPU(s), "
-                                     "rows stored into one shared page-locked framebuffer" if strong else
+                                     "rows stored into shared page-locked framebuffers" if strong else
                                      f"one full frame per GPU per step, {world} GPU(s), no collective"),
-                       "delivered": "RGBA8 frame in page-locked host memory (RayTracerEngine.render's image)"},
+                       "delivered": "RGBA8 frame in page-locked host memory (RayTracerEngine.render's image)",
+                       "in_flight": Q},
             "rays": {"per_step": int(tot[0] / args.steps), "primary_per_step": int(rays_primary) if world == 1 else None,
                      "shadow_traced_per_step": int(tot[3] / args.steps),
                      "shadow_cast_per_step": int(tot[2] / args.steps),
@@ -264,9 +291,12 @@ def main():
                      "note": "value counts shadow rays actually traversed; shadow_cast adds the rays the "
                              "reference casts where N.L <= 0 and discards (value_reference_count)",
                      "secondary_per_step": int(st.secondary_rays) if world == 1 else None},
-            "timing": {"call_ms": round(statistics.mean(calls), 4), "kernel_ms": round(kernel_ms, 4),
-                       "what": "per frame: call_ms = wall time inside rt_render_ex (RenderStats.milliseconds), "
-                               "kernel_ms = HIP events around its launch; ms_per_step - call_ms = Python loop"},
+            "timing": {"in_flight": Q, "submit_to_done_ms": round(statistics.mean(calls), 4),
+                       "kernel_ms": round(kernel_ms, 4),
+                       "what": "frames pipelined with in_flight renders submitted (rt_render_submit) before the "
+                               "oldest is waited for (rt_render_wait); submit_to_done_ms = one frame's latency "
+                               "from its submit to its image complete in host memory (RenderStats.milliseconds); "
+                               "kernel_ms = HIP events around its launch"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gather": gather,

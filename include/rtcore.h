@@ -56,6 +56,7 @@ extern "C" {
 #define RT_ERR_OOM             (-51)
 #define RT_ERR_CANCELLED       (-60)  /* progress callback returned 0                  */
 #define RT_ERR_STACK           (-61)  /* BVH deeper than the traversal stack           */
+#define RT_ERR_BUSY            (-32)  /* RT_MAX_IN_FLIGHT renders submitted and not waited for */
 
 /* ---- scene description (ParsingKit Scene stand-in) ----------------------- */
 typedef struct rt_vec3 { double x, y, z; } rt_vec3;
@@ -201,6 +202,22 @@ int32_t rt_render(rt_scene* scene, int32_t camera_index, int32_t chunk_first, in
 int32_t rt_render_ex(rt_scene* scene, int32_t camera_index, int32_t chunk_first, int32_t chunk_step,
                      double* out_rgb, uint8_t* out_rgba8, uint32_t flags, rt_stats* stats,
                      rt_progress_fn progress, void* user);
+
+/* Asynchronous render: RayTracerEngine.render is `async` (RayTracer.swift:115-131, 137-205),
+ * so a Swift caller may keep several renders in flight (renderAll, BatchRender).
+ * rt_render_submit enqueues the render rt_render_ex(..., flags, ...) would do into PAGE-LOCKED
+ * outputs (rt_host_alloc / rt_host_register; RT_ERR_INVALID_ARG otherwise), returns at once
+ * with *ticket, and the kernels store the image straight into the buffers.  At most
+ * RT_MAX_IN_FLIGHT renders per scene may be submitted and not yet waited for (RT_ERR_BUSY).
+ * Renders in flight overlap on the GPUs: the next frame's tiles fill the compute units the
+ * previous frame's slowest tiles leave idle.  rt_render_wait blocks until that render's
+ * image is complete in the buffers and fills stats (milliseconds from submit to completion).
+ * Scenes with dielectrics, area lights or maxRecursionDepth > 16 are rendered in submission
+ * order.  rt_render_ex with page-locked outputs and no progress callback is submit + wait. */
+#define RT_MAX_IN_FLIGHT 4
+int32_t rt_render_submit(rt_scene* scene, int32_t camera_index, int32_t chunk_first, int32_t chunk_step,
+                         double* out_rgb, uint8_t* out_rgba8, uint32_t flags, int64_t* ticket);
+int32_t rt_render_wait(rt_scene* scene, int64_t ticket, rt_stats* stats);
 
 /* Page-locked host buffers for rt_render outputs (hipHostMalloc, mapped + portable).
  * When out_rgb / out_rgba8 lie inside one such allocation (or a range registered with

@@ -104,6 +104,8 @@ RT_PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.c_int32)
 RT_OK = 0
 RT_ERR_INVALID_CAMERA = -10
 RT_ERR_NO_SCENE = -20
+RT_ERR_BUSY = -32
+RT_MAX_IN_FLIGHT = 4
 RT_ERR_NO_RENDERER = -21
 RT_ERR_INVALID_ARG = -30
 RT_ERR_UNSUPPORTED = -31
@@ -124,7 +126,7 @@ EXPORTED_SYMBOLS = [
     "rt_stats_collect", "rt_rows_for_chunks", "rt_render_device_counted", "rt_last_error", "rt_version",
     "rt_ply_load", "rt_ply_free", "rt_debug_bvh_hash", "rt_debug_host_build",
     "rt_debug_trace_rays", "rt_debug_occluded_rays", "rt_host_alloc", "rt_host_free", "rt_debug_wave_times",
-    "rt_debug_rcp",
+    "rt_debug_rcp", "rt_render_submit", "rt_render_wait",
     "rt_render_ex", "rt_host_register", "rt_host_unregister",
     "rt_scene_file_load", "rt_scene_file_parse", "rt_scene_file_desc", "rt_scene_file_image_name",
     "rt_scene_file_last_error", "rt_scene_file_destroy",
@@ -189,6 +191,11 @@ def bind(lib: C.CDLL) -> C.CDLL:
     lib.rt_debug_wave_times.restype = C.c_int32
     lib.rt_debug_rcp.argtypes = [C.c_int32, c_double_p, c_double_p, c_double_p]
     lib.rt_debug_rcp.restype = C.c_int32
+    lib.rt_render_submit.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, c_double_p, C.POINTER(C.c_uint8),
+                                     C.c_uint32, C.POINTER(C.c_int64)]
+    lib.rt_render_submit.restype = C.c_int32
+    lib.rt_render_wait.argtypes = [C.c_void_p, C.c_int64, C.POINTER(rt_stats)]
+    lib.rt_render_wait.restype = C.c_int32
     lib.rt_debug_bvh_hash.argtypes = [C.c_void_p, C.c_int32]
     lib.rt_debug_bvh_hash.restype = C.c_uint64
     lib.rt_debug_host_build.argtypes = [P(rt_scene_desc), P(C.c_uint64), C.c_int32, c_int32_p, P(rt_scene_info)]

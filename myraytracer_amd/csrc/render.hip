@@ -413,6 +413,19 @@ static int32_t fail(int32_t code, const std::string& msg) { g_err = msg; return 
 
 constexpr int kRenderBlock = 64;    // default threads per render block (block_threads): one wave
 constexpr int kRenderBatches = 8;   // rt_render: chunk batches per replica (progress / overlap granularity)
+// rt_render_submit: renders in flight per scene.  Each has its own stream, counters and events
+// on every replica, so consecutive frames overlap on the GPU: the next frame's tiles fill the
+// compute units the previous frame's slowest tiles leave idle (tools/probe_overlap.py).
+constexpr int kInFlight = RT_MAX_IN_FLIGHT;
+struct Flight {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+    unsigned long long* counters = nullptr;        // device, kCounterWords
+    unsigned long long* host_counters = nullptr;   // pinned (mapped) copy, valid once `done`
+    unsigned long long* host_counters_dev = nullptr;   // its device address
+    bool counters_zero = false;
+    bool used = false;                             // this replica took part in the render
+};
 
 struct DeviceReplica {
     int device = 0;
@@ -447,6 +460,7 @@ struct DeviceReplica {
     std::vector<hipEvent_t> batch_done, batch_copied;
     int64_t bytes = 0;
     WaveBuffers wave;                         // wavefront-pipeline queues (grown on demand)
+    Flight fl[kInFlight];                     // rt_render_submit slots
 };
 
 }  // namespace
@@ -456,6 +470,15 @@ struct rt_scene {
     std::vector<DeviceReplica> devs;
     std::mutex mu;
     double upload_ms = 0;
+    // rt_render_submit bookkeeping: ticket t uses slot t % kInFlight
+    struct Pending {
+        int64_t ticket = -1;
+        bool pending = false;
+        std::chrono::steady_clock::time_point t0;
+        int64_t primary = 0;
+        bool concurrent = true;                   // on the slot's own stream (else the replica stream)
+    } flights[RT_MAX_IN_FLIGHT];
+    int64_t next_ticket = 0;
 };
 
 template <class T>
@@ -478,6 +501,15 @@ static void free_replica(DeviceReplica& r) {
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.counters_ready) (void)hipEventDestroy(r.counters_ready);
     if (r.host_counters) (void)hipHostFree(r.host_counters);
+    for (Flight& f : r.fl) {
+        if (f.stream) (void)hipStreamSynchronize(f.stream);
+        if (f.ev0) (void)hipEventDestroy(f.ev0);
+        if (f.ev1) (void)hipEventDestroy(f.ev1);
+        if (f.done) (void)hipEventDestroy(f.done);
+        if (f.stream) (void)hipStreamDestroy(f.stream);
+        (void)hipFree(f.counters);
+        if (f.host_counters) (void)hipHostFree(f.host_counters);
+    }
     if (r.stream) (void)hipStreamDestroy(r.stream);
     if (r.copy_stream) (void)hipStreamDestroy(r.copy_stream);
     (void)hipFree(r.out_d); (void)hipFree(r.out8_d);
@@ -536,6 +568,16 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
     HIP_TRY(hipEventCreate(&r.ev1));
     HIP_TRY(hipEventCreateWithFlags(&r.counters_ready, hipEventDisableTiming));
     HIP_TRY(hipHostMalloc((void**)&r.host_counters, kCounterWords * sizeof(unsigned long long), hipHostMallocDefault));
+    for (Flight& f : r.fl) {
+        HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreate(&f.ev0));
+        HIP_TRY(hipEventCreate(&f.ev1));
+        HIP_TRY(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
+        HIP_TRY(hipMalloc((void**)&f.counters, kCounterWords * sizeof(unsigned long long)));
+        HIP_TRY(hipHostMalloc((void**)&f.host_counters, kCounterWords * sizeof(unsigned long long),
+                              hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer((void**)&f.host_counters_dev, f.host_counters, 0));
+    }
     return RT_OK;
 }
 
@@ -1028,6 +1070,149 @@ void rt_host_free(void* ptr) {
 }
 
 
+namespace myrt {
+namespace dev {
+// A render's ray counters to page-locked host memory, zeroed behind for the slot's next render:
+// one tiny kernel on the render's stream (a D2H copy + memset would cross to the DMA engine
+// and back between consecutive frames of a stream).
+__global__ void k_counters_out(unsigned long long* counters, unsigned long long* host) {
+    const int i = threadIdx.x;
+    if (i < kCounterWords) {
+        host[i] = counters[i];
+        counters[i] = 0ull;
+    }
+}
+}  // namespace dev
+}  // namespace myrt
+
+// ---- asynchronous renders into page-locked buffers (rt_render_submit / rt_render_wait).
+// One launch per replica on slot (ticket mod kInFlight)'s stream; the kernels store the rows
+// straight into the caller's buffers; the frame's ray counters follow in one async copy into
+// pinned memory and are zeroed behind it.  Called with s->mu held.  *not_pinned: the outputs
+// are not page-locked (rt_render_ex then takes its staged path).
+static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb,
+                           uint8_t* out_rgba8, uint32_t flags, int64_t* ticket, bool* not_pinned) {
+    *not_pinned = false;
+    const rt_camera& C = s->host.cams[cam];
+    const int32_t W = std::max(1, C.width), H = std::max(1, C.height);
+    const bool frame = (flags & RT_RENDER_FRAME_LAYOUT) != 0;
+    const int32_t rows = frame ? H : rt_rows_for_chunks(H, first, step);
+    if (!pinned_range(out_rgb, (size_t)rows * W * 3 * sizeof(double)) || !pinned_range(out_rgba8, (size_t)rows * W * 4)) {
+        *not_pinned = true;
+        return fail(RT_ERR_INVALID_ARG, "rt_render_submit needs page-locked outputs (rt_host_alloc / rt_host_register)");
+    }
+    const int q = (int)(s->next_ticket % kInFlight);
+    rt_scene::Pending& fp = s->flights[q];
+    if (fp.pending)
+        return fail(RT_ERR_BUSY, "too many renders in flight: wait for ticket " + std::to_string(fp.ticket) + " first");
+    const int32_t D = (int32_t)s->devs.size();
+    // dielectrics / area lights / deep recursion (render_full) and the wavefront pipeline use
+    // per-replica scratch buffers: those renders stay on the replica's own stream, in order
+    const bool concurrent = !(s->host.has_dielectric || !s->host.alights.empty() || s->host.max_depth > kMaxDepthGPU) &&
+                            use_megakernel();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int32_t k = 0; k < D; ++k) {
+        DeviceReplica& r = s->devs[k];
+        Flight& f = r.fl[q];
+        f.used = false;
+        const int32_t myFirst = first + k * step, myStep = step * D;
+        if (myFirst >= num_chunks_total(H)) continue;
+        HIP_TRY(hipSetDevice(r.device));
+        double* zrgb = nullptr;
+        uint8_t* zrgba = nullptr;
+        if ((out_rgb && hipHostGetDevicePointer((void**)&zrgb, out_rgb, 0) != hipSuccess) ||
+            (out_rgba8 && hipHostGetDevicePointer((void**)&zrgba, out_rgba8, 0) != hipSuccess)) {
+            (void)hipGetLastError();
+            *not_pinned = true;
+            return fail(RT_ERR_INVALID_ARG, "page-locked outputs are not mapped for this device");
+        }
+        hipStream_t st = concurrent ? f.stream : r.stream;
+        if (!f.counters_zero) HIP_TRY(hipMemsetAsync(f.counters, 0, kCounterWords * sizeof(unsigned long long), st));
+        f.counters_zero = false;
+        HIP_TRY(hipEventRecord(f.ev0, st));
+        RenderParams P = make_params(s, r, cam, myFirst, myStep, zrgb, zrgba);
+        P.counters = f.counters;
+        P.out_first = frame ? 0 : first;
+        P.out_step = frame ? 1 : step;
+        const int32_t rc = launch(s, r, P, st, false);
+        if (rc != RT_OK) return rc;
+        HIP_TRY(hipEventRecord(f.ev1, st));
+        hipLaunchKernelGGL(dev::k_counters_out, dim3(1), dim3(64), 0, st, f.counters, f.host_counters_dev);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(f.done, st));
+        f.counters_zero = true;
+        f.used = true;
+    }
+    const int64_t n = (int64_t)std::sqrt((double)std::max(1, C.num_samples));
+    fp.ticket = s->next_ticket++;
+    fp.pending = true;
+    fp.t0 = t0;
+    fp.primary = (int64_t)rt_rows_for_chunks(H, first, step) * W * n * n;
+    fp.concurrent = concurrent;
+    if (ticket) *ticket = fp.ticket;
+    return RT_OK;
+}
+
+// Wait for `ticket`; the scene lock is released while the host blocks on the GPU.
+static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_t ticket, rt_stats* stats) {
+    const int q = (int)(((ticket % kInFlight) + kInFlight) % kInFlight);
+    rt_scene::Pending& fp = s->flights[q];
+    if (ticket < 0 || !fp.pending || fp.ticket != ticket)
+        return fail(RT_ERR_INVALID_ARG, "unknown ticket, or already waited for");
+    std::vector<std::pair<int, hipEvent_t>> evs;
+    for (auto& r : s->devs)
+        if (r.fl[q].used) evs.emplace_back(r.device, r.fl[q].done);
+    lock.unlock();
+    hipError_t e = hipSuccess;
+    for (auto& de : evs) {
+        if (e == hipSuccess) e = hipSetDevice(de.first);
+        if (e == hipSuccess) e = hipEventSynchronize(de.second);
+    }
+    lock.lock();
+    fp.pending = false;
+    if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("render failed: ") + hipGetErrorString(e));
+    double km = 0;
+    int64_t sh = 0, se = 0, stc = 0;
+    for (auto& r : s->devs) {
+        Flight& f = r.fl[q];
+        if (!f.used) continue;
+        const unsigned long long* c = f.host_counters;
+        sh += (int64_t)c[0]; se += (int64_t)c[1]; stc += (int64_t)c[kCounterShadowTraced];
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, f.ev0, f.ev1);
+        km = std::max(km, (double)ms);
+    }
+    if (stats) {
+        stats->meshes = s->host.n_meshes; stats->triangles = s->host.n_tris;
+        stats->spheres = s->host.n_spheres; stats->planes = s->host.n_planes;
+        stats->primary_rays = fp.primary;
+        stats->shadow_rays = sh; stats->secondary_rays = se; stats->kernel_ms = km;
+        stats->shadow_rays_traced = stc;
+        stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fp.t0).count();
+    }
+    return RT_OK;
+}
+
+int32_t rt_render_submit(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb, uint8_t* out_rgba8,
+                         uint32_t flags, int64_t* ticket) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+    if (s->devs.empty()) return fail(RT_ERR_NO_RENDERER, "Renderer not initialized.");
+    if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
+    if (flags & ~(uint32_t)RT_RENDER_FRAME_LAYOUT) return fail(RT_ERR_INVALID_ARG, "unknown render flags");
+    if (!ticket) return fail(RT_ERR_INVALID_ARG, "ticket is NULL");
+    int32_t rc = check_renderable(s->host, cam);
+    if (rc != RT_OK) return rc;
+    std::lock_guard<std::mutex> lock(s->mu);
+    bool not_pinned = false;
+    return submit_impl(s, cam, first, step, out_rgb, out_rgba8, flags, ticket, &not_pinned);
+}
+
+int32_t rt_render_wait(rt_scene* s, int64_t ticket, rt_stats* stats) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+    std::unique_lock<std::mutex> lock(s->mu);
+    return wait_impl(s, lock, ticket, stats);
+}
+
 // Host-buffer render across all device replicas (Renderer.render + renderRGBA8Async,
 // Object+Extension.swift:52-379, RayTracer.swift:137-205).  Chunk k of the selection goes to
 // replica (k mod D).  Outputs in page-locked memory (rt_host_alloc / rt_host_register) are
@@ -1047,7 +1232,16 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
     if (flags & ~(uint32_t)RT_RENDER_FRAME_LAYOUT) return fail(RT_ERR_INVALID_ARG, "unknown render flags");
     int32_t rc = check_renderable(s->host, cam);
     if (rc != RT_OK) return rc;
-    std::lock_guard<std::mutex> lock(s->mu);
+    std::unique_lock<std::mutex> lock(s->mu);
+    if (!progress && env_int("MYRT_ZEROCOPY", 1, 0, 1) == 1) {
+        // page-locked outputs: one submitted render (the kernels store the rows themselves)
+        int64_t t = -1;
+        bool not_pinned = false;
+        rc = submit_impl(s, cam, first, step, out_rgb, out_rgba8, flags, &t, &not_pinned);
+        if (rc == RT_OK) return wait_impl(s, lock, t, stats);
+        if (!not_pinned && rc != RT_ERR_BUSY) return rc;
+        (void)hipGetLastError();               // pageable outputs (or every slot busy): staged path
+    }
     auto t0 = std::chrono::steady_clock::now();
     const rt_camera& C = s->host.cams[cam];
     const int32_t W = std::max(1, C.width), H = std::max(1, C.height);

@@ -240,6 +240,66 @@ class RayTracerEngine:
                                 A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0, C.byref(st), cb, None))
         return _stats(st)
 
+    def submit_into(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
+                    rgb: Optional[np.ndarray] = None, rgba: Optional[np.ndarray] = None,
+                    frame_layout: bool = False) -> int:
+        """rt_render_submit: enqueue a render into page-locked arrays (pinned_array /
+        register_host) and return its ticket at once; the arrays must stay alive until
+        wait(ticket).  At most A.RT_MAX_IN_FLIGHT renders may be pending (RenderError -32)."""
+        lib = load_library()
+        if not (0 <= camera_index < len(self.scene.cameras)):
+            raise RenderError(A.RT_ERR_INVALID_CAMERA, "Invalid camera index")
+        cam = self.scene.cameras[camera_index]
+        W, H = max(1, int(cam.image_resolution[0])), max(1, int(cam.image_resolution[1]))
+        rows = H if frame_layout else lib.rt_rows_for_chunks(H, chunk_first, chunk_step)
+        for a, ch, dt in ((rgb, 3, np.float64), (rgba, 4, np.uint8)):
+            if a is not None and (a.shape != (rows, W, ch) or a.dtype != dt or not a.flags.c_contiguous):
+                raise ValueError(f"output array must be C-contiguous {dt.__name__}{(rows, W, ch)}, got "
+                                 f"{a.dtype}{a.shape}")
+        t = C.c_int64(-1)
+        _check(lib.rt_render_submit(self._h, camera_index, chunk_first, chunk_step,
+                                    rgb.ctypes.data_as(A.c_double_p) if rgb is not None else None,
+                                    rgba.ctypes.data_as(C.POINTER(C.c_uint8)) if rgba is not None else None,
+                                    A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0, C.byref(t)))
+        return int(t.value)
+
+    def wait(self, ticket: int) -> RenderStats:
+        """rt_render_wait: block until the submitted render is complete in its arrays."""
+        st = A.rt_stats()
+        _check(load_library().rt_render_wait(self._h, ticket, C.byref(st)))
+        return _stats(st)
+
+    def frame_pipeline(self, camera_index: int, chunk_first: int, chunk_step: int, rgbas, frame_layout: bool = True):
+        """Frames rendered with len(rgbas) renders in flight (rt_render_submit / rt_render_wait),
+        frame k into rgbas[k % len(rgbas)], arguments marshalled once.  Returns (submit, wait):
+        submit(k) enqueues frame k and returns its ticket; wait(ticket) returns the raw rt_stats."""
+        for a in rgbas:                                      # validates every buffer once
+            self.wait(self.submit_into(camera_index, chunk_first, chunk_step, None, a, frame_layout))
+        lib = load_library()
+        h = self._h
+        fs, fw = lib.rt_render_submit, lib.rt_render_wait
+        ptrs = [a.ctypes.data_as(C.POINTER(C.c_uint8)) for a in rgbas]
+        flags = A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0
+        t = C.c_int64(-1)
+        pt = C.byref(t)
+        st = A.rt_stats()
+        pst = C.byref(st)
+        keep = list(rgbas)
+
+        def submit(k: int) -> int:
+            rc = fs(h, camera_index, chunk_first, chunk_step, None, ptrs[k % len(ptrs)], flags, pt)
+            if rc != A.RT_OK:
+                _check(rc)
+            assert keep
+            return t.value
+
+        def wait(ticket: int) -> A.rt_stats:
+            rc = fw(h, ticket, pst)
+            if rc != A.RT_OK:
+                _check(rc)
+            return st
+        return submit, wait
+
     def frame_renderer(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
                        rgb: Optional[np.ndarray] = None, rgba: Optional[np.ndarray] = None,
                        frame_layout: bool = False) -> Callable[[], A.rt_stats]:

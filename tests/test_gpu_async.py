@@ -1,0 +1,124 @@
+"""Renders in flight: rt_render_submit / rt_render_wait (the reference's render is async,
+RayTracer.swift:115-131, 137-205; bench.py keeps RT_MAX_IN_FLIGHT frames in flight).
+
+Each submitted render must deliver exactly the image and counts the synchronous rt_render_ex
+delivers (which is itself checked against the oracle, test_gpu_frames.py / test_gpu_parity.py),
+whatever else is in flight: different cameras and chunk selections at once, waits out of order,
+several replicas, and the scenes that stay in submission order (dielectrics, area lights).
+Errors: too many in flight (RT_ERR_BUSY), unknown or repeated tickets, pageable outputs."""
+import copy
+
+import numpy as np
+import pytest
+
+import myraytracer_amd as M
+from myraytracer_amd import _abi as A
+from myraytracer_amd import scenes
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _sync(eng, cam, first, step, H, W):
+    rgb = M.pinned_array((H, W, 3), np.float64)
+    rgba = M.pinned_array((H, W, 4), np.uint8)
+    rgb.fill(-1.0)
+    rgba.fill(0)
+    st = eng.render_into(cam, first, step, rgb=rgb, rgba=rgba, frame_layout=True)
+    return rgb, rgba, st
+
+
+def _two_camera_c2(w=200, h=150):
+    sc = scenes.scaled(scenes.scene_c2(inline=True), w, h)
+    c2 = copy.deepcopy(sc.cameras[0])
+    c2.position = (1.5, 1.0, 3.5)
+    sc.cameras.append(c2)
+    return sc
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_in_flight_renders_match_synchronous_renders(devices):
+    sc = _two_camera_c2()
+    W, H = sc.cameras[0].image_resolution
+    eng = M.RayTracerEngine(sc, devices=devices)
+    jobs = [(0, 0, 1), (1, 0, 1), (0, 1, 3), (1, 2, 2)]      # (camera, chunk_first, chunk_step)
+    want = [_sync(eng, *j, H, W) for j in jobs]
+    outs = [(M.pinned_array((H, W, 3), np.float64), M.pinned_array((H, W, 4), np.uint8)) for _ in jobs]
+    for rgb, rgba in outs:
+        rgb.fill(-1.0)
+        rgba.fill(0)
+    tickets = [eng.submit_into(c, f, s, rgb=o[0], rgba=o[1], frame_layout=True) for (c, f, s), o in zip(jobs, outs)]
+    assert len(set(tickets)) == len(tickets)
+    for k in (2, 0, 3, 1):                                    # out of order
+        st = eng.wait(tickets[k])
+        rgb, rgba, ws = want[k]
+        assert np.array_equal(outs[k][0], rgb) and np.array_equal(outs[k][1], rgba)
+        assert (st.primary_rays, st.shadow_rays, st.shadow_rays_traced) == \
+               (ws.primary_rays, ws.shadow_rays, ws.shadow_rays_traced)
+        assert st.milliseconds > 0 and st.kernel_ms > 0
+    eng.close()
+
+
+def test_pipelined_frames_against_the_oracle():
+    """Many frames in flight through one engine (bench.py's loop), each checked against the
+    oracle: ring of RT_MAX_IN_FLIGHT framebuffers, wait for the oldest before each submit."""
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 160, 120)
+    ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
+    eng = M.RayTracerEngine(sc)
+    Q = A.RT_MAX_IN_FLIGHT
+    fbs = [M.pinned_array((120, 160, 4), np.uint8) for _ in range(Q)]
+    pend = []
+    for k in range(3 * Q + 1):
+        if len(pend) == Q:
+            kk, t = pend.pop(0)
+            st = eng.wait(t)
+            assert np.array_equal(fbs[kk % Q], ref8) and st.shadow_rays == ost.shadow_rays
+        fbs[k % Q].fill(0)
+        pend.append((k, eng.submit_into(0, 0, 1, rgba=fbs[k % Q], frame_layout=True)))
+    for kk, t in pend:
+        eng.wait(t)
+        assert np.array_equal(fbs[kk % Q], ref8)
+    eng.close()
+
+
+def test_ordered_scenes_dielectric_and_area_light():
+    """Dielectrics / area lights take the full trace() kernel with per-replica scratch: their
+    submitted renders run in order on the replica's stream; results equal rt_render_ex."""
+    from test_gpu_features import _area_scene
+    sc = _area_scene(96, 64)                                 # area lights + glass (render_full)
+    W, H = sc.cameras[0].image_resolution
+    eng = M.RayTracerEngine(sc)
+    want = _sync(eng, 0, 0, 1, H, W)
+    outs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(3)]
+    ts = [eng.submit_into(0, 0, 1, rgba=o, frame_layout=True) for o in outs]
+    for t, o in zip(ts, outs):
+        eng.wait(t)
+        assert np.array_equal(o, want[1])
+    eng.close()
+
+
+def test_submit_errors():
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 64, 48)
+    eng = M.RayTracerEngine(sc)
+    Q = A.RT_MAX_IN_FLIGHT
+    outs = [M.pinned_array((48, 64, 4), np.uint8) for _ in range(Q + 1)]
+    ts = [eng.submit_into(0, 0, 1, rgba=outs[k], frame_layout=True) for k in range(Q)]
+    with pytest.raises(M.RenderError) as e:                  # one too many in flight
+        eng.submit_into(0, 0, 1, rgba=outs[Q], frame_layout=True)
+    assert e.value.code == A.RT_ERR_BUSY
+    with pytest.raises(M.RenderError):                       # never submitted
+        eng.wait(ts[-1] + 100)
+    eng.wait(ts[1])
+    with pytest.raises(M.RenderError):                       # already waited for
+        eng.wait(ts[1])
+    with pytest.raises(M.RenderError) as e:                  # pageable output
+        eng.submit_into(0, 0, 1, rgba=np.zeros((48, 64, 4), np.uint8), frame_layout=True)
+    assert e.value.code == A.RT_ERR_INVALID_ARG
+    for t in (ts[0], ts[2], ts[3]):
+        eng.wait(t)
+    # a slot freed by a wait takes the next submit; rt_render_ex still works meanwhile
+    t = eng.submit_into(0, 0, 1, rgba=outs[Q], frame_layout=True)
+    rgb, rgba, _ = _sync(eng, 0, 0, 1, 48, 64)
+    eng.wait(t)
+    assert np.array_equal(outs[Q], rgba)
+    eng.close()

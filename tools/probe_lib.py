@@ -20,23 +20,25 @@ if len(sys.argv) > 2 and sys.argv[2] == "--child":
     s = torch.cuda.current_stream().cuda_stream
     res = []
     NS = int(os.environ.get("PROBE_N", "1"))     # N > 1: the slowest of the N C4 shares (chunks r::N)
+    sel = os.environ.get("PROBE_SEL")            # "first:step": one chunk selection instead
+    shares = [tuple(int(x) for x in sel.split(":"))] if sel else [(r, NS) for r in range(NS)]
     for rep in range(3):
         worst = 0.0
-        for r in range(NS):
+        for r, NS_ in shares:
             for _ in range(3):
-                eng.render_device(out.data_ptr(), 0, r, NS, stream=s)
+                eng.render_device(out.data_ptr(), 0, r, NS_, stream=s)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(20):
-                eng.render_device(out.data_ptr(), 0, r, NS, stream=s)
+                eng.render_device(out.data_ptr(), 0, r, NS_, stream=s)
             e1.record()
             torch.cuda.synchronize()
             worst = max(worst, e0.elapsed_time(e1) / 20)
         res.append(worst)
     import hashlib
     h = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
-    print(f"{cfg} N={NS} {os.path.basename(os.environ['MYRT_LIB'])}: " + " ".join(f"{x:.4f}" for x in res)
+    print(f"{cfg} {sel or f'N={NS}'} {os.path.basename(os.environ['MYRT_LIB'])}: " + " ".join(f"{x:.4f}" for x in res)
           + f" ms  (min {min(res):.4f})  frame sha1 {h}", flush=True)
     sys.exit(0)
 cfg = sys.argv[1]
