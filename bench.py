@@ -220,11 +220,18 @@ def main():
     run(args.steps, per)
     torch.cuda.synchronize()
     t_elapsed = time.perf_counter() - t_begin
-    kms = [a for a, _ in per]
     calls = [b for _, b in per]
     if world > 1:
         dist.barrier()
-    kernel_ms = statistics.mean(kms)
+    # the render kernel's own launch duration (roofline): HIP events around it, one frame at a
+    # time (with frames in flight the event span also covers the overlapped neighbours)
+    one = eng.frame_renderer(0, first, step, rgb=None, rgba=fbs[0], frame_layout=True)
+    sync = []
+    for _ in range(max(5, min(args.steps, 20))):
+        s_ = one()
+        sync.append((s_.kernel_ms, s_.milliseconds))
+    kernel_ms = statistics.mean(a for a, _ in sync)
+    sync_ms = statistics.mean(b for _, b in sync)
 
     t_max = t_elapsed
     tot = np.array([rays_rank, rays_primary + shadow_cast, shadow_cast, shadow_traced], dtype=np.float64) * args.steps
@@ -292,11 +299,12 @@ def main():
                              "reference casts where N.L <= 0 and discards (value_reference_count)",
                      "secondary_per_step": int(st.secondary_rays) if world == 1 else None},
             "timing": {"in_flight": Q, "submit_to_done_ms": round(statistics.mean(calls), 4),
-                       "kernel_ms": round(kernel_ms, 4),
+                       "one_frame_ms": round(sync_ms, 4), "kernel_ms": round(kernel_ms, 4),
                        "what": "frames pipelined with in_flight renders submitted (rt_render_submit) before the "
-                               "oldest is waited for (rt_render_wait); submit_to_done_ms = one frame's latency "
-                               "from its submit to its image complete in host memory (RenderStats.milliseconds); "
-                               "kernel_ms = HIP events around its launch"},
+                               "oldest is waited for (rt_render_wait); submit_to_done_ms = a pipelined frame's "
+                               "latency from submit to image complete in host memory; one_frame_ms = the same for "
+                               "one frame at a time (rt_render_ex, RenderStats.milliseconds); kernel_ms = HIP events "
+                               "around the render launch in those single frames"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gather": gather,
@@ -324,7 +332,8 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
     lib_sha = _lib_sha()
     r = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
          "kernel_ms": round(kernel_ms, 4),
-         "kernel_ms_source": "HIP events around the render launch on its stream, inside rt_render, timed steps"}
+         "kernel_ms_source": "HIP events around the render launch on its stream, inside rt_render, one frame "
+                             "at a time after the timed steps"}
     if prof is not None and world == 1:
         traffic = prof["hbm_bytes_per_launch"]
         r["traffic"] = int(traffic)

@@ -193,14 +193,27 @@ public:
             };
         }
         check(rt_render(scene_, cameraIndex, 0, 1, r.rgb.data(), r.rgba8.data(), &st, cb, &ctx));
-        r.stats.meshes = st.meshes; r.stats.triangles = st.triangles;
-        r.stats.spheres = st.spheres; r.stats.planes = st.planes;
-        r.stats.primary_rays = st.primary_rays; r.stats.shadow_rays = st.shadow_rays;
-        r.stats.secondary_rays = st.secondary_rays;
-        r.stats.rays = st.primary_rays + st.shadow_rays;
-        r.stats.milliseconds = st.milliseconds; r.stats.kernel_ms = st.kernel_ms;
-        r.stats.shadow_rays_traced = st.shadow_rays_traced;
+        r.stats = toStats(st);
         return r;
+    }
+
+    /* The render is `async` in the reference (renderRGBA8Async, RayTracer.swift:137-205): a
+     * caller may keep several in flight.  submit() enqueues a render of camera `cameraIndex`
+     * into page-locked buffers (PinnedBuffer; W*H*4 bytes RGBA8, and/or W*H*3 doubles) that
+     * must stay alive until wait(ticket) returns; at most RT_MAX_IN_FLIGHT renders may be
+     * pending (RenderError RT_ERR_BUSY).  Renders in flight overlap on the GPUs. */
+    int64_t submit(int32_t cameraIndex, uint8_t* pinnedRgba8, double* pinnedRgb = nullptr) {
+        if (!scene_) throw RenderError(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
+        if (cameraIndex < 0 || cameraIndex >= (int32_t)cams_.size())
+            throw RenderError(RT_ERR_INVALID_CAMERA, "Invalid camera index");
+        int64_t t = -1;
+        check(rt_render_submit(scene_, cameraIndex, 0, 1, pinnedRgb, pinnedRgba8, 0u, &t));
+        return t;
+    }
+    RenderStats wait(int64_t ticket) {
+        rt_stats st{};
+        check(rt_render_wait(scene_, ticket, &st));
+        return toStats(st);
     }
 
     /* renderAll(progress:): every camera in order, progress as one fraction over all rows. */
@@ -225,6 +238,15 @@ public:
     }
 
 private:
+    static RenderStats toStats(const rt_stats& st) {
+        RenderStats r;
+        r.meshes = st.meshes; r.triangles = st.triangles; r.spheres = st.spheres; r.planes = st.planes;
+        r.primary_rays = st.primary_rays; r.shadow_rays = st.shadow_rays; r.secondary_rays = st.secondary_rays;
+        r.rays = st.primary_rays + st.shadow_rays;
+        r.milliseconds = st.milliseconds; r.kernel_ms = st.kernel_ms;
+        r.shadow_rays_traced = st.shadow_rays_traced;
+        return r;
+    }
     rt_scene* scene_ = nullptr;
     std::vector<rt_camera> cams_;
     std::vector<CameraMeta> meta_;

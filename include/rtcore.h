@@ -214,7 +214,7 @@ int32_t rt_render_ex(rt_scene* scene, int32_t camera_index, int32_t chunk_first,
  * image is complete in the buffers and fills stats (milliseconds from submit to completion).
  * Scenes with dielectrics, area lights or maxRecursionDepth > 16 are rendered in submission
  * order.  rt_render_ex with page-locked outputs and no progress callback is submit + wait. */
-#define RT_MAX_IN_FLIGHT 4
+#define RT_MAX_IN_FLIGHT 8
 int32_t rt_render_submit(rt_scene* scene, int32_t camera_index, int32_t chunk_first, int32_t chunk_step,
                          double* out_rgb, uint8_t* out_rgba8, uint32_t flags, int64_t* ticket);
 int32_t rt_render_wait(rt_scene* scene, int64_t ticket, rt_stats* stats);

@@ -105,7 +105,7 @@ RT_OK = 0
 RT_ERR_INVALID_CAMERA = -10
 RT_ERR_NO_SCENE = -20
 RT_ERR_BUSY = -32
-RT_MAX_IN_FLIGHT = 4
+RT_MAX_IN_FLIGHT = 8
 RT_ERR_NO_RENDERER = -21
 RT_ERR_INVALID_ARG = -30
 RT_ERR_UNSUPPORTED = -31

@@ -417,12 +417,16 @@ constexpr int kRenderBatches = 8;   // rt_render: chunk batches per replica (pro
 // on every replica, so consecutive frames overlap on the GPU: the next frame's tiles fill the
 // compute units the previous frame's slowest tiles leave idle (tools/probe_overlap.py).
 constexpr int kInFlight = RT_MAX_IN_FLIGHT;
+constexpr int kSubmitDmaDefault = 0;   // rt_render_submit delivery (MYRT_SUBMIT_DMA, submit_impl)
 struct Flight {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     unsigned long long* counters = nullptr;        // device, kCounterWords
     unsigned long long* host_counters = nullptr;   // pinned (mapped) copy, valid once `done`
     unsigned long long* host_counters_dev = nullptr;   // its device address
+    double* stage_rgb = nullptr;                   // device staging of this replica's rows (DMA delivery)
+    uint8_t* stage_rgba = nullptr;
+    int64_t stage_px = 0;
     bool counters_zero = false;
     bool used = false;                             // this replica took part in the render
 };
@@ -508,6 +512,8 @@ static void free_replica(DeviceReplica& r) {
         if (f.done) (void)hipEventDestroy(f.done);
         if (f.stream) (void)hipStreamDestroy(f.stream);
         (void)hipFree(f.counters);
+        (void)hipFree(f.stage_rgb);
+        (void)hipFree(f.stage_rgba);
         if (f.host_counters) (void)hipHostFree(f.host_counters);
     }
     if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -1057,7 +1063,10 @@ int32_t rt_host_alloc(uint64_t bytes, void** out) {
     if (!out) return fail(RT_ERR_INVALID_ARG, "null output pointer");
     *out = nullptr;
     if (bytes == 0) return RT_OK;
-    if (hipHostMalloc(out, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+    // MYRT_HOST_NONCOHERENT=1 (A/B switch): coarse-grained pinned memory
+    const unsigned fl = hipHostMallocMapped | hipHostMallocPortable |
+                        (env_int("MYRT_HOST_NONCOHERENT", 0, 0, 1) ? hipHostMallocNonCoherent : 0u);
+    if (hipHostMalloc(out, bytes, fl) != hipSuccess) {
         (void)hipGetLastError();
         *out = nullptr;
         return fail(RT_ERR_OOM, "hipHostMalloc failed");
@@ -1127,18 +1136,61 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
             return fail(RT_ERR_INVALID_ARG, "page-locked outputs are not mapped for this device");
         }
         hipStream_t st = concurrent ? f.stream : r.stream;
+        // delivery: 0 = the kernel stores the rows into the host buffer; 1 = rows rendered into
+        // device staging and copied by the DMA engine; 2 = staging only, not delivered
+        // (measurement switch MYRT_SUBMIT_DMA)
+        const int dma = env_int("MYRT_SUBMIT_DMA", kSubmitDmaDefault, 0, 2);
+        int32_t nq = 0;
+        for (int32_t c = myFirst; c < num_chunks_total(H); c += myStep) nq++;
+        if (dma) {
+            const int64_t px = (int64_t)nq * 8 * W;
+            if (px > f.stage_px) {
+                (void)hipFree(f.stage_rgb); (void)hipFree(f.stage_rgba);
+                f.stage_rgb = nullptr; f.stage_rgba = nullptr; f.stage_px = 0;
+                HIP_TRY(hipMalloc((void**)&f.stage_rgb, px * 3 * sizeof(double)));
+                HIP_TRY(hipMalloc((void**)&f.stage_rgba, px * 4));
+                f.stage_px = px;
+            }
+        }
         if (!f.counters_zero) HIP_TRY(hipMemsetAsync(f.counters, 0, kCounterWords * sizeof(unsigned long long), st));
         f.counters_zero = false;
-        HIP_TRY(hipEventRecord(f.ev0, st));
-        RenderParams P = make_params(s, r, cam, myFirst, myStep, zrgb, zrgba);
+        const bool timing = env_int("MYRT_SUBMIT_EVENTS", 1, 0, 1) == 1;   // A/B switch
+        if (timing) HIP_TRY(hipEventRecord(f.ev0, st));
+        RenderParams P = make_params(s, r, cam, myFirst, myStep, dma ? (out_rgb ? f.stage_rgb : nullptr) : zrgb,
+                                     dma ? (out_rgba8 ? f.stage_rgba : nullptr) : zrgba);
         P.counters = f.counters;
-        P.out_first = frame ? 0 : first;
-        P.out_step = frame ? 1 : step;
+        if (!dma) {                                      // rows at their places in the caller's buffer
+            P.out_first = frame ? 0 : first;
+            P.out_step = frame ? 1 : step;
+        }                                                // else packed rows of this replica's chunks
         const int32_t rc = launch(s, r, P, st, false);
         if (rc != RT_OK) return rc;
-        HIP_TRY(hipEventRecord(f.ev1, st));
-        hipLaunchKernelGGL(dev::k_counters_out, dim3(1), dim3(64), 0, st, f.counters, f.host_counters_dev);
-        HIP_TRY(hipGetLastError());
+        if (dma == 1) {
+            // chunk q of this replica = selection entry k + q*D = image chunk myFirst + q*myStep;
+            // its 8 rows go to output row 8*(base + q*stride): one 2-D copy for the full chunks
+            const int32_t base = frame ? myFirst : k, stride = frame ? myStep : D;
+            const bool lastPartial = (H % 8) != 0 && myFirst + (nq - 1) * myStep == num_chunks_total(H) - 1;
+            const int32_t nfull = nq - (lastPartial ? 1 : 0);
+            auto copy = [&](void* dst, const void* src, size_t bpp) -> hipError_t {
+                const size_t rowB = (size_t)W * bpp, chunkB = 8 * rowB;
+                hipError_t e = hipSuccess;
+                if (nfull > 0)
+                    e = hipMemcpy2DAsync(static_cast<char*>(dst) + (size_t)base * chunkB, (size_t)stride * chunkB, src,
+                                         chunkB, chunkB, (size_t)nfull, hipMemcpyDeviceToHost, st);
+                if (e == hipSuccess && lastPartial)
+                    e = hipMemcpyAsync(static_cast<char*>(dst) + (size_t)(base + nfull * stride) * chunkB,
+                                       static_cast<const char*>(src) + (size_t)nfull * chunkB, (size_t)(H % 8) * rowB,
+                                       hipMemcpyDeviceToHost, st);
+                return e;
+            };
+            if (out_rgb) HIP_TRY(copy(out_rgb, f.stage_rgb, 3 * sizeof(double)));
+            if (out_rgba8) HIP_TRY(copy(out_rgba8, f.stage_rgba, 4));
+        }
+        if (timing) HIP_TRY(hipEventRecord(f.ev1, st));
+        if (env_int("MYRT_SUBMIT_COUNTERS", 1, 0, 1) == 1) {
+            hipLaunchKernelGGL(dev::k_counters_out, dim3(1), dim3(64), 0, st, f.counters, f.host_counters_dev);
+            HIP_TRY(hipGetLastError());
+        }
         HIP_TRY(hipEventRecord(f.done, st));
         f.counters_zero = true;
         f.used = true;
@@ -1179,7 +1231,7 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
         const unsigned long long* c = f.host_counters;
         sh += (int64_t)c[0]; se += (int64_t)c[1]; stc += (int64_t)c[kCounterShadowTraced];
         float ms = 0;
-        (void)hipEventElapsedTime(&ms, f.ev0, f.ev1);
+        if (hipEventElapsedTime(&ms, f.ev0, f.ev1) != hipSuccess) (void)hipGetLastError();
         km = std::max(km, (double)ms);
     }
     if (stats) {

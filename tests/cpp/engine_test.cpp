@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -245,6 +246,27 @@ static int run_gpu() {
         rt_stats st{};
         myrt::check(rt_render(eng.handle(), 0, 0, 1, pin.data(), nullptr, &st, nullptr, nullptr));
         EXPECT(std::memcmp(pin.data(), r.rgb.data(), r.rgb.size() * sizeof(double)) == 0, "pinned output differs");
+        // renders in flight (submit / wait): every one delivers the same image, waits out of order
+        std::vector<std::unique_ptr<myrt::PinnedBuffer<uint8_t>>> bufs;
+        std::vector<int64_t> tickets;
+        for (int k = 0; k < RT_MAX_IN_FLIGHT; ++k) {
+            bufs.emplace_back(new myrt::PinnedBuffer<uint8_t>((size_t)96 * 64 * 4));
+            std::memset(bufs.back()->data(), 0, bufs.back()->size());
+            tickets.push_back(eng.submit(0, bufs.back()->data()));
+        }
+        try {
+            myrt::PinnedBuffer<uint8_t> more((size_t)96 * 64 * 4);
+            eng.submit(0, more.data());
+            EXPECT(false, "a render past RT_MAX_IN_FLIGHT was accepted");
+        } catch (const myrt::RenderError& e) {
+            EXPECT(e.code == RT_ERR_BUSY, "busy code %d", e.code);
+        }
+        for (int k = RT_MAX_IN_FLIGHT - 1; k >= 0; --k) {
+            const auto ws = eng.wait(tickets[k]);
+            EXPECT(std::memcmp(bufs[k]->data(), r.rgba8.data(), r.rgba8.size()) == 0, "in-flight render %d differs", k);
+            EXPECT(ws.shadow_rays == r.stats.shadow_rays && ws.primary_rays == r.stats.primary_rays,
+                   "in-flight render %d counts", k);
+        }
     }
     {   // a scene file decoded by the library (RayTracerEngine.init(data:)) renders like its descriptor
         auto eng = myrt::RayTracerEngine::fromData(kC1Json, myrt::SceneFormat::Json);

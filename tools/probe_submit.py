@@ -15,18 +15,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
-fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(4)]
-for first, step in ((0, 1), (5, 8)):
-    submit, wait = eng.frame_pipeline(0, first, step, fbs, frame_layout=True)
+fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(8)]
+for (first, step), Q in (((0, 1), 4), ((5, 8), 2), ((5, 8), 4), ((5, 8), 8)):
+    submit, wait = eng.frame_pipeline(0, first, step, fbs[:Q], frame_layout=True)
     for rep in range(2):
         ts, tw, pend = [], [], collections.deque()
         t0 = time.perf_counter()
         for k in range(60):
-            if len(pend) == 4:
+            if len(pend) == Q:
                 a = time.perf_counter(); wait(pend.popleft()); tw.append(time.perf_counter() - a)
             a = time.perf_counter(); pend.append(submit(k)); ts.append(time.perf_counter() - a)
         while pend:
             wait(pend.popleft())
         tot = (time.perf_counter() - t0) * 1e3 / 60
-        print(f"share {first}::{step}: {tot:.4f} ms/frame; submit {np.mean(ts) * 1e3:.4f} ms "
+        print(f"share {first}::{step}, {Q} in flight: {tot:.4f} ms/frame; submit {np.mean(ts) * 1e3:.4f} ms "
               f"(p90 {np.percentile(ts, 90) * 1e3:.4f}), wait {np.mean(tw) * 1e3:.4f} ms", flush=True)

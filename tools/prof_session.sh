@@ -4,7 +4,7 @@
 #   -> gpurun_out/TAG_*/ (rocprofv3 output) and gpurun_out/TAG_roofline.json (tools/pmc_roofline.py)
 set -u
 tag="$1"; shift
-B="python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-side-paths $*"
+B="python3 bench.py --steps 20 --warmup 3 --in-flight 1 --no-cpu-baseline --no-side-paths $*"
 K="${KERNEL:-render_kernel<false, false, true>}"
 steps=(
   "${tag}_trace|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_trace -- $B"
