@@ -69,8 +69,11 @@ def parse():
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong (default): one frame per step split over the ranks (C4); "
                         "weak: every rank renders a full frame per step")
-    p.add_argument("--in-flight", type=int, default=4,
-                   help="renders in flight (rt_render_submit); 1 = one synchronous frame at a time")
+    p.add_argument("--in-flight", type=int, default=0,
+                   help="renders in flight (rt_render_submit); 1 = one frame at a time; 0 = 4, or 8 for a "
+                        "strong split over N > 1 GPUs")
+    p.add_argument("--hw-queues", type=int, default=0,
+                   help="GPU_MAX_HW_QUEUES for this process (0 = HIP's default; 8 for a strong split over N > 1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-side-paths", action="store_true", help="skip the fp64 / device-only side measurements")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share (OMP_NUM_THREADS / affinity)")
@@ -132,6 +135,16 @@ def main():
         sys.exit(relaunch_under_torchrun(args))
     if "WORLD_SIZE" in os.environ and world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # renders in flight: a small C4 share's frames overlap best when each in-flight render has a
+    # hardware queue of its own (tools/probe_submit.py: N=8 share 0.155 -> 0.12 ms/frame with 8
+    # queues and 8 in flight; the whole C3 frame gains nothing from more than HIP's default 4).
+    # Set before anything initialises HIP; the HIP default otherwise.
+    if args.in_flight <= 0:
+        args.in_flight = 8 if (args.gpus > 1 and args.scaling == "strong") else 4
+    if args.hw_queues <= 0 and args.gpus > 1 and args.scaling == "strong":
+        args.hw_queues = 8
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 
     import numpy as np
     import torch
@@ -290,7 +303,7 @@ def main():
                                      "rows stored into shared page-locked framebuffers" if strong else
                                      f"one full frame per GPU per step, {world} GPU(s), no collective"),
                        "delivered": "RGBA8 frame in page-locked host memory (RayTracerEngine.render's image)",
-                       "in_flight": Q},
+                       "in_flight": Q, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default")},
             "rays": {"per_step": int(tot[0] / args.steps), "primary_per_step": int(rays_primary) if world == 1 else None,
                      "shadow_traced_per_step": int(tot[3] / args.steps),
                      "shadow_cast_per_step": int(tot[2] / args.steps),
