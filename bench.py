@@ -72,8 +72,8 @@ def parse():
     p.add_argument("--in-flight", type=int, default=0,
                    help="renders in flight (rt_render_submit); 1 = one frame at a time; 0 = 4, or 8 for a "
                         "strong split over N > 1 GPUs")
-    p.add_argument("--hw-queues", type=int, default=0,
-                   help="GPU_MAX_HW_QUEUES for this process (0 = HIP's default; 8 for a strong split over N > 1)")
+    p.add_argument("--hw-queues", type=int, default=-1,
+                   help="GPU_MAX_HW_QUEUES for this process (-1 = 16, one per render in flight; 0 = HIP's default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-side-paths", action="store_true", help="skip the fp64 / device-only side measurements")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share (OMP_NUM_THREADS / affinity)")
@@ -135,14 +135,14 @@ def main():
         sys.exit(relaunch_under_torchrun(args))
     if "WORLD_SIZE" in os.environ and world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    # renders in flight: a small C4 share's frames overlap best when each in-flight render has a
-    # hardware queue of its own (tools/probe_submit.py: N=8 share 0.155 -> 0.12 ms/frame with 8
-    # queues and 8 in flight; the whole C3 frame gains nothing from more than HIP's default 4).
-    # Set before anything initialises HIP; the HIP default otherwise.
+    # renders in flight overlap only on hardware queues of their own: HIP's default of 4 queues
+    # per process is shared by the library's streams (tools/probe_submit.py: a C4/8 share takes
+    # 0.155 / 0.12 / 0.095 ms per frame with 4 / 8 / 16 queues and 8 in flight; the whole C3
+    # frame 0.678 -> 0.665 ms with 16).  Set before anything initialises HIP.
     if args.in_flight <= 0:
         args.in_flight = 8 if (args.gpus > 1 and args.scaling == "strong") else 4
-    if args.hw_queues <= 0 and args.gpus > 1 and args.scaling == "strong":
-        args.hw_queues = 8
+    if args.hw_queues < 0:
+        args.hw_queues = 16
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 
