@@ -75,6 +75,40 @@ def test_c3_full_frame_bench_path(c3_ply, monkeypatch):
     eng.close()
 
 
+def test_c3_full_frames_in_flight_bench_path(c3_ply, monkeypatch):
+    """bench.py's timed loop exactly: frames submitted with 4 renders in flight
+    (engine.frame_pipeline -> rt_render_submit / rt_render_wait), frame k into page-locked
+    framebuffer k mod 4; every delivered frame equals the oracle's RGBA8 and its counts."""
+    import collections
+    monkeypatch.delenv("MYRT_PATH", raising=False)
+    sc, ref, ref8, ost = c3_ply
+    eng = M.RayTracerEngine(sc)
+    H, W = ref.shape[:2]
+    fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(4)]
+    submit, wait = eng.frame_pipeline(0, 0, 1, fbs, frame_layout=True)
+    pend = collections.deque()
+    done = 0
+
+    def check(k, st):
+        _assert_frame(None, fbs[k % 4], ref, ref8)
+        assert st.shadow_rays == ost.shadow_rays and st.shadow_rays_traced == ost.shadow_rays_used
+        fbs[k % 4].fill(0)
+
+    for k in range(10):
+        if len(pend) == 4:
+            kk, t = pend.popleft()
+            check(kk, wait(t))
+            done += 1
+        fbs[k % 4].fill(0) if k < 4 else None
+        pend.append((k, submit(k)))
+    while pend:
+        kk, t = pend.popleft()
+        check(kk, wait(t))
+        done += 1
+    assert done == 10
+    eng.close()
+
+
 def test_c3_full_frame_device_path(c3_ply, monkeypatch):
     import torch
     monkeypatch.delenv("MYRT_PATH", raising=False)
