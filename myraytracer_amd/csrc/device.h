@@ -208,12 +208,22 @@ struct Stack {
     name.top_n = 0;                                                  \
     name.sp = 0
 
+// Near-root records in LDS (MYRT_LDS_TOP, measured slower) and the runtime switch of the scalar
+// path (MYRT_SCALAR=0) are compiled out of production builds: each kept a value live in SGPRs
+// across the walk, and the kernel spills SGPRs to VGPR lanes (v_readlane in the inner step).
+#ifndef MYRT_LDS_TOP_CODE
+#define MYRT_LDS_TOP_CODE 0
+#endif
+#ifndef MYRT_SCALAR_RUNTIME
+#define MYRT_SCALAR_RUNTIME 0
+#endif
+constexpr bool MYRT_LDS_TOP_CODE_ON = MYRT_LDS_TOP_CODE != 0;
 // Copy compact records [0, n) into this wave's LDS slab (n <= kLdsTopMax), for Stack::top.  Every lane copies records lane, lane+64, ...; LDS operations of one wave
 // complete in order, so the wave's later reads see them (the barrier orders the waves of
 // multi-wave blocks, which each copy their own slab).
 // Called by every lane of the block (it holds a barrier); the slabs follow the stacks.
 __device__ __forceinline__ const lds_crec* stage_top_records(const RenderParams& P, unsigned long long* lds_base) {
-    const int n = P.lds_top_n;
+    const int n = MYRT_LDS_TOP_CODE ? P.lds_top_n : 0;
     if (n <= 0) return nullptr;
     lds_crec* slab = (lds_crec*)(lds_u64*)(lds_base + (size_t)blockDim.x * kLds) + (size_t)(threadIdx.x >> 6) * n * 4;
     const f32x4* src = reinterpret_cast<const f32x4*>(P.crecs);
@@ -604,7 +614,7 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
 #ifndef MYRT_SCALAR_WREC
 #define MYRT_SCALAR_WREC 1      // measured: C3 -0.5 %, C5 -0.5 % with MYRT_HIT2
 #endif
-    if (P.scalar_nodes && __all(ref == r0)) {
+    if ((MYRT_SCALAR_RUNTIME ? P.scalar_nodes != 0 : true) && __all(ref == r0)) {
         if (COUNT && !P.count_ref)
             c.it_wave_scalar[SHADOW] += ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) ? 1 : 0;
         // MYRT_SCALAR_WREC: the wave-uniform step reads the FP64 record (no v_cvt_f64_f32)
@@ -631,7 +641,7 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
         c.div_lanes += 1;
         c.div_distinct += ((int)(threadIdx.x & 63) == my_leader) ? 1 : 0;
     }
-    if (ref < st.top_n) {                    // near-root record: this wave's LDS copy
+    if (MYRT_LDS_TOP_CODE && ref < st.top_n) {   // near-root record: this wave's LDS copy
         const lds_crec* q = st.top + 4 * ref;
         const f32x4 a = q[0], b = q[1], e = q[2];
         // the refs are read as integers: bit-casting elements of a float vector read every

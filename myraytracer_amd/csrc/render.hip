@@ -764,8 +764,10 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         const char* te = std::getenv("MYRT_CTRI");              // A/B switch: MYRT_CTRI=0
         P.ctris = (S.compact_tris && !(te && te[0] == '0')) ? r.ctris : nullptr;
         // near-root records in LDS (megakernel; launch() clears it for the other kernels)
-        P.lds_top_n = (int32_t)std::min<int64_t>(env_int("MYRT_LDS_TOP", kLdsTopDefault, 0, kLdsTopMax),
-                                                 std::min<int64_t>(S.lds_top_records, P.compact_limit));
+        P.lds_top_n = dev::MYRT_LDS_TOP_CODE_ON
+                          ? (int32_t)std::min<int64_t>(env_int("MYRT_LDS_TOP", kLdsTopDefault, 0, kLdsTopMax),
+                                                       std::min<int64_t>(S.lds_top_records, P.compact_limit))
+                          : 0;
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
