@@ -294,6 +294,12 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                                     ((unsigned)(unsigned char)cz << 16) | (255u << 24);
             reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
         }
+#if MYRT_WAVE_TIMES >= 2
+        if (P.wave_times && P.out_rgb) {        // debug: per-lane walk iterations instead of the colour
+            P.out_rgb[o * 3 + 0] = (double)cnt.it_closest;
+            P.out_rgb[o * 3 + 1] = (double)cnt.it_shadow;
+        }
+#endif
     }
 #if MYRT_WAVE_TIMES
     if (P.wave_times) {                                              // debug timeline
