@@ -70,10 +70,10 @@ def parse():
                    help="strong (default): one frame per step split over the ranks (C4); "
                         "weak: every rank renders a full frame per step")
     p.add_argument("--in-flight", type=int, default=0,
-                   help="renders in flight (rt_render_submit); 1 = one frame at a time; 0 = 4, or 8 for a "
-                        "strong split over N > 1 GPUs")
+                   help="renders in flight (rt_render_submit); 1 = one frame at a time; 0 = RT_MAX_IN_FLIGHT (16)")
     p.add_argument("--hw-queues", type=int, default=-1,
-                   help="GPU_MAX_HW_QUEUES for this process (-1 = 16, one per render in flight; 0 = HIP's default)")
+                   help="GPU_MAX_HW_QUEUES for this process (-1 = 32: one per render in flight and the "
+                        "library's own streams; 0 = HIP's default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-side-paths", action="store_true", help="skip the fp64 / device-only side measurements")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share (OMP_NUM_THREADS / affinity)")
@@ -137,12 +137,15 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     # renders in flight overlap only on hardware queues of their own: HIP's default of 4 queues
     # per process is shared by the library's streams (tools/probe_submit.py: a C4/8 share takes
-    # 0.155 / 0.12 / 0.095 ms per frame with 4 / 8 / 16 queues and 8 in flight; the whole C3
-    # frame 0.678 -> 0.665 ms with 16).  Set before anything initialises HIP.
+    # 0.155 / 0.12 / 0.095 ms per frame with 4 / 8 / 16 queues and 8 in flight;
+    # tools/probe_shares.py: 0.086 ms with 32 queues and 16 in flight, the whole C3 frame
+    # 0.642 ms).  Set before anything initialises HIP.
     if args.in_flight <= 0:
-        args.in_flight = 8 if (args.gpus > 1 and args.scaling == "strong") else 4
+        args.in_flight = 16
     if args.hw_queues < 0:
-        args.hw_queues = 16
+        # ranks rehearsed on one GPU (MYRT_BENCH_DEVICE) share its hardware queue slots: more
+        # than 32 queues on one GPU time-slice (2 ranks x 32: 10.6 ms per frame instead of 0.35)
+        args.hw_queues = 32 // (world if "MYRT_BENCH_DEVICE" in os.environ else 1)
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 

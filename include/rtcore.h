@@ -199,6 +199,9 @@ int32_t rt_render(rt_scene* scene, int32_t camera_index, int32_t chunk_first, in
  * selections (other devices, other processes sharing one registered buffer) thereby
  * gather one image with no copy.  rt_render(...) == rt_render_ex(..., 0, ...). */
 #define RT_RENDER_FRAME_LAYOUT  1u
+/* rt_render_submit: time the render kernels with HIP events (rt_stats.kernel_ms of
+ * rt_render_wait; 0 without the flag).  rt_render / rt_render_ex always time them. */
+#define RT_RENDER_KERNEL_TIME   2u
 int32_t rt_render_ex(rt_scene* scene, int32_t camera_index, int32_t chunk_first, int32_t chunk_step,
                      double* out_rgb, uint8_t* out_rgba8, uint32_t flags, rt_stats* stats,
                      rt_progress_fn progress, void* user);
@@ -214,7 +217,7 @@ int32_t rt_render_ex(rt_scene* scene, int32_t camera_index, int32_t chunk_first,
  * image is complete in the buffers and fills stats (milliseconds from submit to completion).
  * Scenes with dielectrics, area lights or maxRecursionDepth > 16 are rendered in submission
  * order.  rt_render_ex with page-locked outputs and no progress callback is submit + wait. */
-#define RT_MAX_IN_FLIGHT 8
+#define RT_MAX_IN_FLIGHT 16
 int32_t rt_render_submit(rt_scene* scene, int32_t camera_index, int32_t chunk_first, int32_t chunk_step,
                          double* out_rgb, uint8_t* out_rgba8, uint32_t flags, int64_t* ticket);
 int32_t rt_render_wait(rt_scene* scene, int64_t ticket, rt_stats* stats);

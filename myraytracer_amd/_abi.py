@@ -61,6 +61,7 @@ class rt_scene_desc(C.Structure):
 
 
 RT_RENDER_FRAME_LAYOUT = 1
+RT_RENDER_KERNEL_TIME = 2
 RT_SCENE_FORMAT_AUTO, RT_SCENE_FORMAT_JSON, RT_SCENE_FORMAT_XML = 0, 1, 2
 
 
@@ -105,7 +106,7 @@ RT_OK = 0
 RT_ERR_INVALID_CAMERA = -10
 RT_ERR_NO_SCENE = -20
 RT_ERR_BUSY = -32
-RT_MAX_IN_FLIGHT = 8
+RT_MAX_IN_FLIGHT = 16
 RT_ERR_NO_RENDERER = -21
 RT_ERR_INVALID_ARG = -30
 RT_ERR_UNSUPPORTED = -31

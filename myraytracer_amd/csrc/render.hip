@@ -430,6 +430,7 @@ struct Flight {
     unsigned long long* counters = nullptr;        // device, kCounterWords
     unsigned long long* host_counters = nullptr;   // pinned (mapped) copy, valid once `done`
     unsigned long long* host_counters_dev = nullptr;   // its device address
+    bool timed = false;                            // ev0/ev1 recorded for the slot's current render
     double* stage_rgb = nullptr;                   // device staging of this replica's rows (DMA delivery)
     uint8_t* stage_rgba = nullptr;
     int64_t stage_px = 0;
@@ -1110,6 +1111,9 @@ __global__ void k_counters_out(unsigned long long* counters, unsigned long long*
 static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step, double* out_rgb,
                            uint8_t* out_rgba8, uint32_t flags, int64_t* ticket, bool* not_pinned) {
     *not_pinned = false;
+    // kernel timing events only when asked for (rt_render_ex always asks): each is a packet
+    // on the stream, ~1 us of a C4/8 share's 85 us per frame (tools/probe_shares.py)
+    const bool timing = (flags & RT_RENDER_KERNEL_TIME) != 0 && env_int("MYRT_SUBMIT_EVENTS", 1, 0, 1) == 1;
     const rt_camera& C = s->host.cams[cam];
     const int32_t W = std::max(1, C.width), H = std::max(1, C.height);
     const bool frame = (flags & RT_RENDER_FRAME_LAYOUT) != 0;
@@ -1162,8 +1166,8 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         }
         if (!f.counters_zero) HIP_TRY(hipMemsetAsync(f.counters, 0, kCounterWords * sizeof(unsigned long long), st));
         f.counters_zero = false;
-        const bool timing = env_int("MYRT_SUBMIT_EVENTS", 1, 0, 1) == 1;   // A/B switch
         if (timing) HIP_TRY(hipEventRecord(f.ev0, st));
+        f.timed = timing;
         RenderParams P = make_params(s, r, cam, myFirst, myStep, dma ? (out_rgb ? f.stage_rgb : nullptr) : zrgb,
                                      dma ? (out_rgba8 ? f.stage_rgba : nullptr) : zrgba);
         P.counters = f.counters;
@@ -1239,7 +1243,7 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
         const unsigned long long* c = f.host_counters;
         sh += (int64_t)c[0]; se += (int64_t)c[1]; stc += (int64_t)c[kCounterShadowTraced];
         float ms = 0;
-        if (hipEventElapsedTime(&ms, f.ev0, f.ev1) != hipSuccess) (void)hipGetLastError();
+        if (f.timed && hipEventElapsedTime(&ms, f.ev0, f.ev1) != hipSuccess) (void)hipGetLastError();
         km = std::max(km, (double)ms);
     }
     if (stats) {
@@ -1258,7 +1262,8 @@ int32_t rt_render_submit(rt_scene* s, int32_t cam, int32_t first, int32_t step, 
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
     if (s->devs.empty()) return fail(RT_ERR_NO_RENDERER, "Renderer not initialized.");
     if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
-    if (flags & ~(uint32_t)RT_RENDER_FRAME_LAYOUT) return fail(RT_ERR_INVALID_ARG, "unknown render flags");
+    if (flags & ~(uint32_t)(RT_RENDER_FRAME_LAYOUT | RT_RENDER_KERNEL_TIME))
+        return fail(RT_ERR_INVALID_ARG, "unknown render flags");
     if (!ticket) return fail(RT_ERR_INVALID_ARG, "ticket is NULL");
     int32_t rc = check_renderable(s->host, cam);
     if (rc != RT_OK) return rc;
@@ -1297,7 +1302,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
         // page-locked outputs: one submitted render (the kernels store the rows themselves)
         int64_t t = -1;
         bool not_pinned = false;
-        rc = submit_impl(s, cam, first, step, out_rgb, out_rgba8, flags, &t, &not_pinned);
+        rc = submit_impl(s, cam, first, step, out_rgb, out_rgba8, flags | RT_RENDER_KERNEL_TIME, &t, &not_pinned);
         if (rc == RT_OK) return wait_impl(s, lock, t, stats);
         if (!not_pinned && rc != RT_ERR_BUSY) return rc;
         (void)hipGetLastError();               // pageable outputs (or every slot busy): staged path

@@ -242,10 +242,11 @@ class RayTracerEngine:
 
     def submit_into(self, camera_index: int = 0, chunk_first: int = 0, chunk_step: int = 1,
                     rgb: Optional[np.ndarray] = None, rgba: Optional[np.ndarray] = None,
-                    frame_layout: bool = False) -> int:
+                    frame_layout: bool = False, kernel_time: bool = False) -> int:
         """rt_render_submit: enqueue a render into page-locked arrays (pinned_array /
         register_host) and return its ticket at once; the arrays must stay alive until
-        wait(ticket).  At most A.RT_MAX_IN_FLIGHT renders may be pending (RenderError -32)."""
+        wait(ticket).  At most A.RT_MAX_IN_FLIGHT renders may be pending (RenderError -32).
+        kernel_time: time the kernels with HIP events (RenderStats.kernel_ms, else 0)."""
         lib = load_library()
         if not (0 <= camera_index < len(self.scene.cameras)):
             raise RenderError(A.RT_ERR_INVALID_CAMERA, "Invalid camera index")
@@ -260,7 +261,8 @@ class RayTracerEngine:
         _check(lib.rt_render_submit(self._h, camera_index, chunk_first, chunk_step,
                                     rgb.ctypes.data_as(A.c_double_p) if rgb is not None else None,
                                     rgba.ctypes.data_as(C.POINTER(C.c_uint8)) if rgba is not None else None,
-                                    A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0, C.byref(t)))
+                                    (A.RT_RENDER_FRAME_LAYOUT if frame_layout else 0) |
+                                    (A.RT_RENDER_KERNEL_TIME if kernel_time else 0), C.byref(t)))
         return int(t.value)
 
     def wait(self, ticket: int) -> RenderStats:

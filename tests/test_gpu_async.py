@@ -47,7 +47,9 @@ def test_in_flight_renders_match_synchronous_renders(devices):
     for rgb, rgba in outs:
         rgb.fill(-1.0)
         rgba.fill(0)
-    tickets = [eng.submit_into(c, f, s, rgb=o[0], rgba=o[1], frame_layout=True) for (c, f, s), o in zip(jobs, outs)]
+    # every other render asks for kernel timing (RT_RENDER_KERNEL_TIME)
+    tickets = [eng.submit_into(c, f, s, rgb=o[0], rgba=o[1], frame_layout=True, kernel_time=(k % 2 == 0))
+               for k, ((c, f, s), o) in enumerate(zip(jobs, outs))]
     assert len(set(tickets)) == len(tickets)
     for k in (2, 0, 3, 1):                                    # out of order
         st = eng.wait(tickets[k])
@@ -55,7 +57,8 @@ def test_in_flight_renders_match_synchronous_renders(devices):
         assert np.array_equal(outs[k][0], rgb) and np.array_equal(outs[k][1], rgba)
         assert (st.primary_rays, st.shadow_rays, st.shadow_rays_traced) == \
                (ws.primary_rays, ws.shadow_rays, ws.shadow_rays_traced)
-        assert st.milliseconds > 0 and st.kernel_ms > 0
+        assert st.milliseconds > 0
+        assert (st.kernel_ms > 0) if k % 2 == 0 else (st.kernel_ms == 0)
     eng.close()
 
 

@@ -18,7 +18,9 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 sc = (scenes.scene_c3 if cfg == "c3" else scenes.scene_c5)(path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
-Q = 8
+QS = [int(x) for x in os.environ.get("PROBE_Q", "1,4,8").split(",")]
+NS = [int(x) for x in os.environ.get("PROBE_N", "2,4,8").split(",")]
+Q = max(QS + [4])
 fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
 K = 40
 
@@ -40,10 +42,10 @@ def t_pipe(first, step, q):
     return (time.perf_counter() - t) * 1e3 / K
 
 
-full = {q: t_pipe(0, 1, q) for q in (1, 2, 4, 8)}
+full = {q: t_pipe(0, 1, q) for q in sorted(set(QS + [4]))}
 print("full frame ms: " + ", ".join(f"{q} in flight {v:.4f}" for q, v in full.items()), flush=True)
-for n in (2, 4, 8):
-    for q in (1, 4, 8):
+for n in NS:
+    for q in QS:
         worst = max(t_pipe(r, n, q) for r in range(n))
         print(f"N={n} {q} in flight: slowest share {worst:.4f} ms/frame -> {full[q] / worst:.2f}x of the same "
               f"pipeline on 1 GPU (eff {full[q] / (n * worst):.3f}); vs 1 GPU at 4 in flight "
