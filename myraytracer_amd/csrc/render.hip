@@ -158,7 +158,12 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 __device__ __forceinline__ unsigned long long pixel_seed(int i, int j) {
     return (((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull;
 }
-constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;   // x, y, z, rng.state (8 B x 64 lanes each)
+constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;
+#ifndef MYRT_TILE_W
+#define MYRT_TILE_W 8        // megakernel tile width in pixels (8: 8x8 tiles; 16: 16x4; 32: 32x2)
+#endif
+constexpr int kTileW = MYRT_TILE_W;
+static_assert(kTileW == 8 || kTileW == 16 || kTileW == 32, "MYRT_TILE_W: 8, 16 or 32");   // x, y, z, rng.state (8 B x 64 lanes each)
 typedef __attribute__((address_space(3))) double lds_f64;
 #if MYRT_MEGA_WPE > 0
 #define MYRT_MEGA_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_MEGA_WPE)))
@@ -179,20 +184,21 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 #if MYRT_WAVE_TIMES
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    // one tile = (8 x waves-per-block) x 8 pixels of one selected chunk (one 8x8 square per
-    // wave); tiles are row-major over (slot, column)
+    // one tile = (TW x waves-per-block) x TH pixels of one selected chunk (one TW x TH
+    // rectangle per wave, TW = MYRT_TILE_W); tiles are row-major over (slot, band, column)
+    constexpr int TW = kTileW, TH = 64 / kTileW, BANDS = 8 / TH;
     const int wpb = (int)(blockDim.x >> 6);
-    const int gx = (P.cam.width + 8 * wpb - 1) / (8 * wpb);
+    const int gx = (P.cam.width + TW * wpb - 1) / (TW * wpb);
     int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
     // rotated dispatch order: the first rot_slots chunk rows go last (host: MYRT_ROTATE)
     if (P.rot_slots > 0) {
-        tile += P.rot_slots * gx;
+        tile += P.rot_slots * gx * BANDS;
         if (tile >= (int)gridDim.x) tile -= (int)gridDim.x;
     }
-    const int i = (tile % gx) * (8 * wpb) + wave * 8 + (lane & 7);
-    const int slot = tile / gx;                        // position in the selected chunk list
+    const int i = (tile % gx) * (TW * wpb) + wave * TW + (lane % TW);
+    const int slot = tile / (gx * BANDS);              // position in the selected chunk list
     const int chunk = P.chunk_first + slot * P.chunk_step;
-    const int rowInChunk = lane >> 3;
+    const int rowInChunk = ((tile / gx) % BANDS) * TH + lane / TW;
     const int j = chunk * 8 + rowInChunk;
     const DCamera& C = P.cam;
     const bool valid = (i < C.width) && (j < C.height);
@@ -807,9 +813,10 @@ static int block_threads() {
     const int v = e ? std::atoi(e) : kRenderBlock;
     return (v == 64 || v == 128 || v == 256) ? v : kRenderBlock;
 }
-static dim3 render_grid(const RenderParams& P, int threads) {
-    const int px = 8 * (threads / 64);                   // pixels per block along a row
-    return dim3((unsigned)(((P.cam.width + px - 1) / px) * P.num_chunks), 1, 1);
+// blocks of `threads` lanes over the selected chunks, one tw x (64/tw) tile per wave
+static dim3 render_grid(const RenderParams& P, int threads, int tw = 8) {
+    const int px = tw * (threads / 64);                  // pixels per block along a row
+    return dim3((unsigned)(((P.cam.width + px - 1) / px) * (8 / (64 / tw)) * P.num_chunks), 1, 1);
 }
 
 static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count) {
@@ -881,7 +888,7 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         return RT_OK;
     }
     const int bt = block_threads();
-    dim3 grid = render_grid(P, bt);
+    dim3 grid = render_grid(P, bt, dev::kTileW);
     dim3 block((unsigned)bt, 1, 1);
     const size_t lds = (size_t)dev::kLds * bt * sizeof(int2) + (size_t)(bt / 64) * P.lds_top_n * sizeof(CRec) +
                        (size_t)dev::kPixSlots * bt * sizeof(double);
@@ -1738,7 +1745,7 @@ int32_t rt_debug_wave_times(rt_scene* s, int32_t slot, int32_t cam, int32_t firs
     HIP_TRY(hipSetDevice(r.device));
     RenderParams P = make_params(s, r, cam, first, step, d_out_rgb, nullptr);
     const int bt = block_threads();
-    const int64_t waves = (int64_t)render_grid(P, bt).x * (bt / 64);
+    const int64_t waves = (int64_t)render_grid(P, bt, dev::kTileW).x * (bt / 64);
     if (waves > r.wave_times_cap) {
         (void)hipFree(r.wave_times); r.wave_times = nullptr; r.wave_times_cap = 0;
         HIP_TRY(hipMalloc((void**)&r.wave_times, (size_t)waves * 3 * sizeof(unsigned long long)));
