@@ -63,8 +63,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip ta
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    # 2000 C3 frames = ~1.3 s timed at N = 1: long enough for an outside GPU-busy sampler
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong (default): one frame per step split over the ranks (C4); "
