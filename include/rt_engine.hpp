@@ -201,13 +201,15 @@ public:
      * caller may keep several in flight.  submit() enqueues a render of camera `cameraIndex`
      * into page-locked buffers (PinnedBuffer; W*H*4 bytes RGBA8, and/or W*H*3 doubles) that
      * must stay alive until wait(ticket) returns; at most RT_MAX_IN_FLIGHT renders may be
-     * pending (RenderError RT_ERR_BUSY).  Renders in flight overlap on the GPUs. */
-    int64_t submit(int32_t cameraIndex, uint8_t* pinnedRgba8, double* pinnedRgb = nullptr) {
+     * pending (RenderError RT_ERR_BUSY).  Renders in flight overlap on the GPUs.
+     * kernelTime: time the kernels with HIP events (RenderStats::kernel_ms, else 0). */
+    int64_t submit(int32_t cameraIndex, uint8_t* pinnedRgba8, double* pinnedRgb = nullptr, bool kernelTime = false) {
         if (!scene_) throw RenderError(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
         if (cameraIndex < 0 || cameraIndex >= (int32_t)cams_.size())
             throw RenderError(RT_ERR_INVALID_CAMERA, "Invalid camera index");
         int64_t t = -1;
-        check(rt_render_submit(scene_, cameraIndex, 0, 1, pinnedRgb, pinnedRgba8, 0u, &t));
+        check(rt_render_submit(scene_, cameraIndex, 0, 1, pinnedRgb, pinnedRgba8,
+                               kernelTime ? RT_RENDER_KERNEL_TIME : 0u, &t));
         return t;
     }
     RenderStats wait(int64_t ticket) {
