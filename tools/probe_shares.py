@@ -1,6 +1,7 @@
 """Per-share frame time of an N-GPU C4 split rendered on one GPU (every rank's share, not only
 the slowest), with the host time spent inside rt_render_submit / rt_render_wait, to separate
-share imbalance from per-frame overhead.  Env: PROBE_N (default 8), PROBE_Q (16), PROBE_K (200)."""
+share imbalance from per-frame overhead.  Env: PROBE_N (default 8), PROBE_Q (16), PROBE_K (200),
+PROBE_CFG (c3 / c5)."""
 import collections
 import os
 import sys
@@ -13,7 +14,8 @@ import myraytracer_amd as M
 from myraytracer_amd import scenes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache"))
+CFG = os.environ.get("PROBE_CFG", "c3")
+sc = (scenes.scene_c3 if CFG == "c3" else scenes.scene_c5)(path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
 N = int(os.environ.get("PROBE_N", "8"))
