@@ -152,12 +152,24 @@ struct Stack {
     int stride;
 #endif
     int sp;
+    // uni_spill (MYRT_UNIFORM_SPILL): test once per wave whether any lane is past the LDS
+    // part; when none is (nearly always), the push/pop is a plain LDS access with no per-lane
+    // exec masking around the private-memory branch.  A compile-time constant per kernel
+    // (everything here is inlined): on in the primary-ray megakernel (C3 -0.9 %), off where
+    // it raised register spills (bounce megakernel: C5 +2 %)
+#ifndef MYRT_UNIFORM_SPILL
+#define MYRT_UNIFORM_SPILL 1
+#endif
+    bool uni_spill;
+    __device__ __forceinline__ bool lds_only() const { return MYRT_UNIFORM_SPILL && uni_spill && !__any(sp >= kLds); }
     __device__ __forceinline__ static unsigned long long pack(int ref, double t) {
         return (unsigned long long)(unsigned)ref | ((unsigned long long)(unsigned)__double2hiint(t) << 32);
     }
     __device__ __forceinline__ void push(int ref, double t) {
         const unsigned long long e = pack(ref, t);
-        if (sp < kLds) {
+        if (lds_only()) {
+            lds[sp * stride] = e;
+        } else if (sp < kLds) {
             lds[sp * stride] = e;
         } else {
             asm volatile("" ::: "memory");   // keep the two stores apart (no select-of-pointers)
@@ -169,7 +181,9 @@ struct Stack {
     // rare spill store is conditional
     __device__ __forceinline__ void push_if(bool keep, int ref, double t) {
         const unsigned long long e = pack(ref, t);
-        if (sp < kLds) {
+        if (lds_only()) {
+            lds[sp * stride] = e;
+        } else if (sp < kLds) {
             lds[sp * stride] = e;
         } else if (keep) {
             asm volatile("" ::: "memory");
@@ -180,10 +194,15 @@ struct Stack {
     // returns the ref; `tlo` = lower bound of the entry distance
     __device__ __forceinline__ int pop(double& tlo) {
         --sp;
-        unsigned long long e = lds[min(sp, kLds - 1) * stride];   // unconditional ds_read
-        if (sp >= kLds) {
-            asm volatile("" ::: "memory");
-            e = spill[sp - kLds];
+        unsigned long long e;
+        if (lds_only()) {
+            e = lds[sp * stride];
+        } else {
+            e = lds[min(sp, kLds - 1) * stride];   // unconditional ds_read
+            if (sp >= kLds) {
+                asm volatile("" ::: "memory");
+                e = spill[sp - kLds];
+            }
         }
         tlo = __hiloint2double((int)(unsigned)(e >> 32), 0);
         return (int)(unsigned)(e & 0xffffffffull);
@@ -206,6 +225,7 @@ struct Stack {
     name.spill = (priv_u64*)(name##_spill_mem);                      \
     name.top = nullptr;                                              \
     name.top_n = 0;                                                  \
+    name.uni_spill = false;                                          \
     name.sp = 0
 
 // Near-root records in LDS (MYRT_LDS_TOP, measured slower) and the runtime switch of the scalar

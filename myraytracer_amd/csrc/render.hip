@@ -211,6 +211,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 #endif
     if (valid) {
         MYRT_STACK(st, lds_stack);
+        st.uni_spill = !BOUNCE;
         st.top = top;
         st.top_n = P.lds_top_n;
         PCG32 rng(pixel_seed(i, j));
