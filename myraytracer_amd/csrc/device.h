@@ -127,7 +127,7 @@ __device__ __forceinline__ int xcd_tile(int b, int nb, int G) {
 // the low mantissa word truncates toward zero, i.e. rounds a positive distance DOWN, so
 // pop-time culling stays conservative (negative distances are never culled).
 #ifndef MYRT_KLDS
-#define MYRT_KLDS 16
+#define MYRT_KLDS 8
 #endif
 constexpr int kLds = MYRT_KLDS;
 #ifndef MYRT_STRIDE64

@@ -165,8 +165,14 @@ constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;
 constexpr int kTileW = MYRT_TILE_W;
 static_assert(kTileW == 8 || kTileW == 16 || kTileW == 32, "MYRT_TILE_W: 8, 16 or 32");   // x, y, z, rng.state (8 B x 64 lanes each)
 typedef __attribute__((address_space(3))) double lds_f64;
+#ifndef MYRT_BOUNCE_UNI_SPILL
+#define MYRT_BOUNCE_UNI_SPILL 0   // wave-uniform LDS-only stack push/pop in the bounce kernel too
+#endif
+#ifndef MYRT_BOUNCE_WPE
+#define MYRT_BOUNCE_WPE 6   // the bounce (mirror/conductor) instantiation: 6 waves/SIMD (80 VGPRs; C5 -7.5 %)
+#endif
 #if MYRT_MEGA_WPE > 0
-#define MYRT_MEGA_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_MEGA_WPE)))
+#define MYRT_MEGA_ATTR __attribute__((amdgpu_waves_per_eu(BOUNCE ? MYRT_BOUNCE_WPE : MYRT_MEGA_WPE)))
 #else
 #define MYRT_MEGA_ATTR
 #endif
@@ -211,7 +217,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 #endif
     if (valid) {
         MYRT_STACK(st, lds_stack);
-        st.uni_spill = !BOUNCE;
+        st.uni_spill = !BOUNCE || MYRT_BOUNCE_UNI_SPILL;
         st.top = top;
         st.top_n = P.lds_top_n;
         PCG32 rng(pixel_seed(i, j));
