@@ -208,6 +208,8 @@ def main():
     # render is async, RayTracer.swift:137-205), arguments marshalled once (engine.frame_pipeline)
     submit, wait = eng.frame_pipeline(0, first, step, fbs, frame_layout=True)
 
+    submit_s = [0.0]                                  # host time inside rt_render_submit (timed frames)
+
     def run(k_frames, stats_out=None):
         pend = collections.deque()
         for k in range(k_frames):
@@ -215,7 +217,12 @@ def main():
                 s_ = wait(pend.popleft())
                 if stats_out is not None:
                     stats_out.append((s_.kernel_ms, s_.milliseconds))
-            pend.append(submit(k))
+            if stats_out is not None:
+                ts = time.perf_counter()
+                pend.append(submit(k))
+                submit_s[0] += time.perf_counter() - ts
+            else:
+                pend.append(submit(k))
         last = None
         while pend:
             last = wait(pend.popleft())
@@ -252,6 +259,19 @@ def main():
 
     t_max = t_elapsed
     tot = np.array([rays_rank, rays_primary + shadow_cast, shadow_cast, shadow_traced], dtype=np.float64) * args.steps
+    per_rank = None
+    if world > 1:
+        # every rank's own clock and host submit cost, so an N > 1 line shows its imbalance
+        mine = torch.tensor([t_elapsed * 1e3 / args.steps, submit_s[0] * 1e6 / args.steps, float(rows)],
+                            dtype=torch.float64)
+        allr = [torch.zeros(3, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        ms_r = [round(float(x[0]), 4) for x in allr]
+        per_rank = {"ms_per_step": ms_r, "submit_us_per_frame": [round(float(x[1]), 2) for x in allr],
+                    "rows": [int(x[2]) for x in allr], "min_ms": min(ms_r), "max_ms": max(ms_r),
+                    "imbalance": round(max(ms_r) / max(1e-9, min(ms_r)), 4),
+                    "what": "per rank: its own timed-region clock per frame (value uses the max), host time "
+                            "inside rt_render_submit per frame, rows of the frame it renders"}
     if world > 1:
         tt = torch.tensor([t_elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -315,7 +335,9 @@ def main():
                      "note": "value counts shadow rays actually traversed; shadow_cast adds the rays the "
                              "reference casts where N.L <= 0 and discards (value_reference_count)",
                      "secondary_per_step": int(st.secondary_rays) if world == 1 else None},
+            "per_rank": per_rank,
             "timing": {"in_flight": Q, "submit_to_done_ms": round(statistics.mean(calls), 4),
+                       "submit_us_per_frame": round(submit_s[0] * 1e6 / args.steps, 2),
                        "one_frame_ms": round(sync_ms, 4), "kernel_ms": round(kernel_ms, 4),
                        "what": "frames pipelined with in_flight renders submitted (rt_render_submit) before the "
                                "oldest is waited for (rt_render_wait); submit_to_done_ms = a pipelined frame's "
@@ -367,6 +389,25 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
                     "td_busy = TD_TD_BUSY_sum/256 / (GRBM_GUI_ACTIVE/8); both from the same profile",
             "executed_load_bytes": int(load_bytes),
             "executed_load_GBs": round(load_bytes / (kernel_ms * 1e-3) / 1e9, 1)}
+    # the pipelined loop's own per-frame GPU time: rocprofv3 --kernel-trace of this bench's timed
+    # frames (16 in flight), union of the render launches' intervals per frame
+    # (tools/overlap_session.sh + tools/overlap_summary.py -> profiles/overlap_<config>.json)
+    opath = os.path.join(ROOT, "profiles", f"overlap_{args.config}.json")
+    if os.path.exists(opath) and world == 1:
+        with open(opath) as fh:
+            ov = json.load(fh)
+        pl = {"union_per_frame_ms": ov["union_per_frame_ms"], "concurrency": ov["concurrency"],
+              "max_overlap": ov["max_overlap"], "idle_fraction_of_span": ov["idle_fraction_of_span"],
+              "trace_bench_ms_per_step": ov.get("bench_ms_per_step"),
+              "source": os.path.relpath(opath, ROOT),
+              "profile_build_matches": ov.get("lib_sha256_16") == lib_sha,
+              "what": "render launches of the timed frames under rocprofv3 --kernel-trace: union of their "
+                      "[start, end) per frame (the GPU time a pipelined frame costs), mean launches running "
+                      "at once, most at once; achieved = HBM bytes per launch / union per frame"}
+        if r["traffic"] is not None:
+            pl["achieved"] = round(r["traffic"] / (ov["union_per_frame_ms"] * 1e-3) / 1e9, 2)
+            pl["frac"] = round(pl["achieved"] / HBM_PEAK_GBS, 4)
+        r["pipelined"] = pl
     r["reference_work"] = {
         "what": "SURVEY.md 8(d) algorithmic bytes of the reference's unpruned walk (56 N_node + 72 N_tri + "
                 "72 N_smooth + 24 N_px), counted on the GPU in reference order; most are cache hits, so the "
@@ -434,21 +475,39 @@ def side_paths(eng, first, step, rows, W, H, rays_rank, args):
     return res
 
 
+def cgroup_cpu_quota():
+    """CPUs the process may actually use: the cgroup v2 CPU quota (cpu.max = "quota period",
+    or "max") - on the GPU box 1600000/100000 = 16 CPUs while the affinity mask shows all 256
+    cores of the machine (profiles/r03a_cpu_probe.txt)."""
+    path = "/sys/fs/cgroup/cpu.max"
+    try:
+        with open(path) as fh:
+            raw = fh.read().strip()
+    except OSError:
+        return None, path, None
+    q, _, per = raw.partition(" ")
+    if q == "max" or not per:
+        return None, path, raw
+    import math
+    return max(1, math.ceil(int(q) / int(per))), path, raw
+
+
 def cpu_threads(args):
-    if args.cpu_threads:
-        return args.cpu_threads
-    share = len(os.sched_getaffinity(0))
-    omp = os.environ.get("OMP_NUM_THREADS")          # the pool's CPU share per GPU (16 on the box)
-    if omp and omp.isdigit():
-        share = min(share, int(omp))
-    return max(1, share)
+    """Threads for the CPU baseline: the cores this process can really run on = min(affinity,
+    cgroup quota).  Returns (threads, evidence)."""
+    aff = len(os.sched_getaffinity(0))
+    quota, qpath, raw = cgroup_cpu_quota()
+    usable = min(aff, quota) if quota else aff
+    ev = {"affinity": aff, "cgroup_cpu_max": raw, "cgroup_source": qpath, "cgroup_quota_cpus": quota,
+          "usable_cores": usable, "nproc": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    return (args.cpu_threads or usable), ev
 
 
 def cpu_baseline(scene, H, args):
     """Oracle (C++ restatement of the reference CPU renderer): median over whole frames at the
     CPU share (one task per 8-row chunk, Object+Extension.swift:285-360), plus 1 thread."""
     import oracle
-    cores = cpu_threads(args)
+    cores, evidence = cpu_threads(args)
     t0 = time.time()
     o = oracle.OracleScene(scene if scene.objects[0].ply_path is None else _inline(scene))
     build_s = time.time() - t0
@@ -467,9 +526,10 @@ def cpu_baseline(scene, H, args):
     return {"value": round(med, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
             "frames": [round(x, 3) for x in rates], "spread": round((max(rates) - min(rates)) / med, 3),
             "one_thread": round(statistics.median(one), 4),
-            "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
-            "sample": f"median of {len(rates)} whole frames ({px} px each) on {cores} threads (the GPU box's "
-                      f"CPU share: OMP_NUM_THREADS; nproc reports the whole machine); one_thread = every "
+            "cores_evidence": evidence,
+            "sample": f"median of {len(rates)} whole frames ({px} px each) on {cores} threads = the cores this "
+                      f"process may use (min of the affinity mask and the cgroup CPU quota, cores_evidence); "
+                      f"one_thread = every "
                       f"{stride}th 8-row chunk on 1 thread, {len(one)} runs; rays = primary + shadow cast; "
                       f"oracle BVH build {build_s:.1f}s excluded"}
 

@@ -39,6 +39,14 @@
 
 #include <stdint.h>
 
+/* ABI version of this header (rt_version() reports it).
+ *   1: round-1/2 layout.
+ *   2: rt_object gained `num_normals` (sizeof(rt_object), the stride of rt_scene_desc.objects,
+ *      changed: callers built against version 1 must be rebuilt).  A non-NULL `normals` now
+ *      requires num_normals == num_positions; version-1 callers that left it 0 get
+ *      RT_ERR_INVALID_ARG instead of an unchecked read. */
+#define RT_ABI_VERSION 2
+
 #ifdef __cplusplus
 extern "C" {
 #endif

@@ -37,7 +37,7 @@ def _stale(target, sources):
 def build_product(force: bool = False) -> str:
     out = os.path.join(PKG, "libmyrt.so")
     srcs = [os.path.join(CSRC, s) for s in PRODUCT_SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in ("layout.h", "scene.h", "device.h", "wavefront.h", "slab32.h", "render_full.h")] + [os.path.join(ROOT, "include", "rtcore.h")]
+    deps = srcs + [os.path.join(CSRC, h) for h in ("layout.h", "scene.h", "device.h", "wavefront.h", "render_full.h")] + [os.path.join(ROOT, "include", "rtcore.h")]
     if force or _stale(out, deps):
         _run([HIPCC, "--offload-arch=gfx950", *COMMON_FLAGS, "-o", out, *srcs])
     return out

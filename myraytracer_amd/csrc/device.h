@@ -5,7 +5,6 @@
 #include <hip/hip_runtime.h>
 
 #include "layout.h"
-#include "slab32.h"
 
 namespace myrt {
 namespace dev {
@@ -80,6 +79,14 @@ __device__ __forceinline__ double slab(double lx, double ly, double lz, double h
 // PCG32 (Object+Extension.swift:556-589)
 struct PCG32 {
     unsigned long long state, inc;
+    PCG32() = default;
+    // a stream resumed at `state` (PCG32(seed) sets inc = seed << 1 | 1)
+    __device__ static PCG32 resume(unsigned long long state, unsigned long long seed) {
+        PCG32 r;
+        r.state = state;
+        r.inc = (seed << 1) | 1ull;
+        return r;
+    }
     __device__ explicit PCG32(unsigned long long seed) {
         state = 0ull; inc = (seed << 1) | 1ull;
         (void)next();
@@ -130,27 +137,16 @@ __device__ __forceinline__ int xcd_tile(int b, int nb, int G) {
 #define MYRT_KLDS 8
 #endif
 constexpr int kLds = MYRT_KLDS;
-#ifndef MYRT_STRIDE64
-#define MYRT_STRIDE64 1      // per-wave LDS slab with a constant stride of 64 (shift, not multiply)
-#endif
 constexpr int kSpill = kStackCap - kLds;   // the host refuses deeper scenes (scene.cpp, RT_ERR_STACK)
 static_assert(kSpill > 0, "LDS part larger than the stack");
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 typedef __attribute__((address_space(5))) unsigned long long priv_u64;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) f32x4 lds_crec;   // a CRec = 4 consecutive f32x4
-typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
 struct Stack {
-    lds_u64* lds;        // &lds_base[threadIdx.x]; stride blockDim.x (MYRT_STRIDE64: per-wave slab, stride 64)
+    lds_u64* lds;        // this lane's column of the wave's [kLds][64] LDS slab
     priv_u64* spill;     // kSpill private entries
-    const lds_crec* top; // this wave's LDS copy of compact records [0, top_n) (render kernels)
-    int top_n;           // 0 = no LDS records
-#if MYRT_STRIDE64
+    // per-wave slab with a constant stride of 64: a slot address is a shift, not a multiply
+    // by blockDim.x (C3/C5 -1 %)
     static constexpr int stride = 64;
-#else
-    int stride;
-#endif
     int sp;
     // uni_spill (MYRT_UNIFORM_SPILL): test once per wave whether any lane is past the LDS
     // part; when none is (nearly always), the push/pop is a plain LDS access with no per-lane
@@ -210,50 +206,13 @@ struct Stack {
     // drop every entry above `base`
     __device__ __forceinline__ void reset(int base) { sp = base; }
 };
-#if MYRT_STRIDE64
-#define MYRT_STACK_LDS(name, lds_base) \
-    name.lds = (lds_u64*)((lds_base) + (threadIdx.x >> 6) * (kLds * 64) + (threadIdx.x & 63))
-#else
-#define MYRT_STACK_LDS(name, lds_base) \
-    name.lds = (lds_u64*)((lds_base) + threadIdx.x);                 \
-    name.stride = blockDim.x
-#endif
 #define MYRT_STACK(name, lds_base)                                   \
     unsigned long long name##_spill_mem[kSpill];                     \
     Stack name;                                                      \
-    MYRT_STACK_LDS(name, lds_base);                                  \
+    name.lds = (lds_u64*)((lds_base) + (threadIdx.x >> 6) * (kLds * 64) + (threadIdx.x & 63)); \
     name.spill = (priv_u64*)(name##_spill_mem);                      \
-    name.top = nullptr;                                              \
-    name.top_n = 0;                                                  \
     name.uni_spill = false;                                          \
     name.sp = 0
-
-// Near-root records in LDS (MYRT_LDS_TOP, measured slower) and the runtime switch of the scalar
-// path (MYRT_SCALAR=0) are compiled out of production builds: each kept a value live in SGPRs
-// across the walk, and the kernel spills SGPRs to VGPR lanes (v_readlane in the inner step).
-#ifndef MYRT_LDS_TOP_CODE
-#define MYRT_LDS_TOP_CODE 0
-#endif
-#ifndef MYRT_SCALAR_RUNTIME
-#define MYRT_SCALAR_RUNTIME 0
-#endif
-constexpr bool MYRT_LDS_TOP_CODE_ON = MYRT_LDS_TOP_CODE != 0;
-// Copy compact records [0, n) into this wave's LDS slab (n <= kLdsTopMax), for Stack::top.  Every lane copies records lane, lane+64, ...; LDS operations of one wave
-// complete in order, so the wave's later reads see them (the barrier orders the waves of
-// multi-wave blocks, which each copy their own slab).
-// Called by every lane of the block (it holds a barrier); the slabs follow the stacks.
-__device__ __forceinline__ const lds_crec* stage_top_records(const RenderParams& P, unsigned long long* lds_base) {
-    const int n = MYRT_LDS_TOP_CODE ? P.lds_top_n : 0;
-    if (n <= 0) return nullptr;
-    lds_crec* slab = (lds_crec*)(lds_u64*)(lds_base + (size_t)blockDim.x * kLds) + (size_t)(threadIdx.x >> 6) * n * 4;
-    const f32x4* src = reinterpret_cast<const f32x4*>(P.crecs);
-    for (int k = threadIdx.x & 63; k < n; k += 64) {
-        const f32x4 a = src[4 * k], b = src[4 * k + 1], c = src[4 * k + 2], d = src[4 * k + 3];
-        slab[4 * k] = a; slab[4 * k + 1] = b; slab[4 * k + 2] = c; slab[4 * k + 3] = d;
-    }
-    __syncthreads();
-    return slab;
-}
 
 // Work counters (COUNT instantiations only).  recs/tris/normals/insts = work this kernel
 // executed.  With RenderParams::count_ref set, the COUNT walk instead follows the
@@ -298,11 +257,8 @@ __device__ __forceinline__ bool slab_hit(double lx, double ly, double lz, double
     if (FAST) {
         tmin = fmax(fmax(mnx, mny), mnz);
         tmax = fmin(mxx, fmin(mxy, mxz));
-#ifndef MYRT_HIT2
-#define MYRT_HIT2 1
-#endif
-        // no NaN here, so tmax >= max(tmin, eps) <=> tmax >= tmin && tmax >= eps
-        hit = MYRT_HIT2 ? (tmax >= tmin && tmax >= eps) : (tmax >= fmax(tmin, eps));
+        // no NaN here, so tmax >= max(tmin, eps) <=> tmax >= tmin && tmax >= eps (two compares)
+        hit = tmax >= tmin && tmax >= eps;
     } else {
         tmin = smax(smax(mnx, mny), mnz);
         tmax = smin(mxx, smin(mxy, mxz));
@@ -313,47 +269,6 @@ __device__ __forceinline__ bool slab_hit(double lx, double ly, double lz, double
 }
 __device__ __forceinline__ bool finite3(const V3& a) {
     return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
-}
-
-// Near/far planes picked by the direction's sign (MYRT_NEARSEL).  In a FAST walk every 1/d is
-// finite and no slab value is NaN, and a box has lo <= hi, so (lo - o)*i <= (hi - o)*i when
-// i >= 0 and >= when i < 0 (IEEE rounding is monotone): simd.min/max of the two slab values
-// (hitAABB, RTContext.swift:557-565) is the near/far plane's value itself, up to the sign of
-// a zero, which no later comparison sees.  Choosing the planes first replaces the six FP64
-// min/max of a box by selects of the (float or SGPR) bounds.
-//   SEL 0: min/max (slab_hit); 1: per-lane selects; 2: wave-uniform octant `soct` (bit a set
-//   when 1/d_a < 0) - the selects of SGPR-held bounds are then scalar.
-#ifndef MYRT_NEARSEL
-#define MYRT_NEARSEL 0      // measured slower (DESIGN §4 lost experiments)
-#endif
-template <bool FAST, int SEL, class T>
-__device__ __forceinline__ bool slab_hit_sel(T lx, T ly, T lz, T hx, T hy, T hz, const V3& o, const V3& inv,
-                                             double eps, int soct, double& tmin_out) {
-    if (!FAST || SEL == 0)
-        return slab_hit<FAST>((double)lx, (double)ly, (double)lz, (double)hx, (double)hy, (double)hz, o, inv, eps,
-                              tmin_out);
-    bool sx, sy, sz;
-    if (SEL == 1) {
-        sx = inv.x < 0.0; sy = inv.y < 0.0; sz = inv.z < 0.0;
-    } else {
-        sx = (soct & 1) != 0; sy = (soct & 2) != 0; sz = (soct & 4) != 0;
-    }
-    const T nx = sx ? hx : lx, ny = sy ? hy : ly, nz = sz ? hz : lz;
-    const T fx = sx ? lx : hx, fy = sy ? ly : hy, fz = sz ? lz : hz;
-    const double tnx = ((double)nx - o.x) * inv.x, tny = ((double)ny - o.y) * inv.y,
-                 tnz = ((double)nz - o.z) * inv.z;
-    const double tfx = ((double)fx - o.x) * inv.x, tfy = ((double)fy - o.y) * inv.y,
-                 tfz = ((double)fz - o.z) * inv.z;
-    const double tmin = fmax(fmax(tnx, tny), tnz);
-    const double tmax = fmin(tfx, fmin(tfy, tfz));
-    tmin_out = tmin;
-    return tmax >= tmin && tmax >= eps;          // no NaN: = tmax >= max(tmin, eps)
-}
-// The wave's common octant of 1/d (bit a set when 1/d_a < 0), or -1 when its lanes differ.
-__device__ __forceinline__ int wave_octant(const V3& inv) {
-    const int oct = (inv.x < 0.0 ? 1 : 0) | (inv.y < 0.0 ? 2 : 0) | (inv.z < 0.0 ? 4 : 0);
-    const int o0 = __builtin_amdgcn_readfirstlane(oct);
-    return __all(oct == o0) ? o0 : -1;
 }
 
 // Triangle geometry from either record format (layout.h TriRec / CTri).
@@ -485,15 +400,15 @@ __device__ __forceinline__ bool prim_shadow(int kind, const TriRec& T, const V3&
 // (true), or the caller must pop (false).  Order = near first, ties to L (the reference
 // pushes R then L after `if d1 > d2 swap`, RTContext.swift:600-606); the far child is
 // pushed.  Children beyond `lim` (conservative t-pruning) count as misses.
-template <bool COUNT, bool FAST, bool SHADOW, int SEL = 0, class Rec>
+template <bool COUNT, bool FAST, bool SHADOW, class Rec>
 __device__ __forceinline__ bool inner_step_rec(const RenderParams& P, const Rec& R, int& ref, const V3& o,
-                                               const V3& inv, double lim, Stack& st, Counts& c, int soct = -1) {
+                                               const V3& inv, double lim, Stack& st, Counts& c) {
     if (COUNT) c.recs++;
     double t0, t1;
-    bool h0 = slab_hit_sel<FAST, SEL>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
-                                      P.eps, soct, t0);
-    bool h1 = slab_hit_sel<FAST, SEL>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
-                                      P.eps, soct, t1);
+    bool h0 = slab_hit<FAST>((double)R.lo[0][0], (double)R.lo[0][1], (double)R.lo[0][2], (double)R.hi[0][0],
+                             (double)R.hi[0][1], (double)R.hi[0][2], o, inv, P.eps, t0);
+    bool h1 = slab_hit<FAST>((double)R.lo[1][0], (double)R.lo[1][1], (double)R.lo[1][2], (double)R.hi[1][0],
+                             (double)R.hi[1][1], (double)R.hi[1][2], o, inv, P.eps, t1);
     h0 = h0 && !(t0 > lim);
     h1 = h1 && !(t1 > lim);
     const int a = R.ref[0], b = R.ref[1];
@@ -567,87 +482,19 @@ __device__ __forceinline__ SRec load_rec_scalar(const WRec* pv) {
     return R;
 }
 
-struct SCRec {                       // a CRec held in SGPRs
-    float lo[2][3], hi[2][3];
-    int ref[2];
-};
-__device__ __forceinline__ float lo_f(unsigned long long q) { return __builtin_bit_cast(float, (unsigned)q); }
-__device__ __forceinline__ float hi_f(unsigned long long q) { return __builtin_bit_cast(float, (unsigned)(q >> 32)); }
-__device__ __forceinline__ SCRec load_crec_scalar(const CRec* pv) {
-    const unsigned long long av = (unsigned long long)pv;
-    const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
-    const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
-    const CRec* p = (const CRec*)((unsigned long long)alo | ((unsigned long long)ahi << 32));
-    // 64-bit outputs: element extraction from a 16-dword ext_vector SGPR output was
-    // miscompiled (all float/int elements read as element 0); register pairs are not
-    unsigned long long q0, q1, q2, q3, q4, q5, q6;
-    asm volatile(
-        "s_load_dwordx2 %0, %7, 0x0\n\t"
-        "s_load_dwordx2 %1, %7, 0x8\n\t"
-        "s_load_dwordx2 %2, %7, 0x10\n\t"
-        "s_load_dwordx2 %3, %7, 0x18\n\t"
-        "s_load_dwordx2 %4, %7, 0x20\n\t"
-        "s_load_dwordx2 %5, %7, 0x28\n\t"
-        "s_load_dwordx2 %6, %7, 0x30\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&s"(q0), "=&s"(q1), "=&s"(q2), "=&s"(q3), "=&s"(q4), "=&s"(q5), "=&s"(q6)
-        : "s"(p));
-    SCRec R;
-    R.lo[0][0] = lo_f(q0); R.lo[0][1] = hi_f(q0); R.lo[0][2] = lo_f(q1);
-    R.lo[1][0] = hi_f(q1); R.lo[1][1] = lo_f(q2); R.lo[1][2] = hi_f(q2);
-    R.hi[0][0] = lo_f(q3); R.hi[0][1] = hi_f(q3); R.hi[0][2] = lo_f(q4);
-    R.hi[1][0] = hi_f(q4); R.hi[1][1] = lo_f(q5); R.hi[1][2] = hi_f(q5);
-    R.ref[0] = (int)(unsigned)q6;
-    R.ref[1] = (int)(unsigned)(q6 >> 32);
-    return R;
-}
-
-#ifndef MYRT_CREC56
-#define MYRT_CREC56 0
-#endif
-// The 56 used bytes of a compact record (3 x dwordx4 + dwordx2; the 8 pad bytes are not
-// fetched): 12.5% less data through the texture-data path per vector record load.
-__device__ __forceinline__ CRec load_crec56(const CRec* p) {
-    const float4* q = reinterpret_cast<const float4*>(p);
-    const float4 a = q[0], b = q[1], e = q[2];
-    const int2 r = *reinterpret_cast<const int2*>(q + 3);
-    CRec R;
-    R.lo[0][0] = a.x; R.lo[0][1] = a.y; R.lo[0][2] = a.z; R.lo[1][0] = a.w;
-    R.lo[1][1] = b.x; R.lo[1][2] = b.y; R.hi[0][0] = b.z; R.hi[0][1] = b.w;
-    R.hi[0][2] = e.x; R.hi[1][0] = e.y; R.hi[1][1] = e.z; R.hi[1][2] = e.w;
-    R.ref[0] = r.x; R.ref[1] = r.y;
-    return R;
-}
-
 // One inner record: compact (float32 bounds, exact) below P.compact_limit, else full;
 // through the scalar cache when the whole wave is at this node.
 template <bool COUNT, bool FAST, bool SHADOW>
 __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, const V3& o, const V3& inv, double lim,
-                                           Stack& st, Counts& c, int soct = -1) {
-    // float bounds in VGPRs: per-lane selects cost what the FP64 min/max they replace cost
-    // (v_cndmask_b32 issues in 4 cycles here, tools/valu_rates.hip; C3 0.769 vs 0.733 ms)
-    constexpr int kLaneSel = MYRT_NEARSEL >= 2 ? 1 : 0;
+                                           Stack& st, Counts& c) {
     const int r0 = __builtin_amdgcn_readfirstlane(ref);
-#ifndef MYRT_SCALAR_FULL
-#define MYRT_SCALAR_FULL 1
-#endif
-#ifndef MYRT_SCALAR_WREC
-#define MYRT_SCALAR_WREC 1      // measured: C3 -0.5 %, C5 -0.5 % with MYRT_HIT2
-#endif
-    if ((MYRT_SCALAR_RUNTIME ? P.scalar_nodes != 0 : true) && __all(ref == r0)) {
+    if (__all(ref == r0)) {
         if (COUNT && !P.count_ref)
             c.it_wave_scalar[SHADOW] += ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) ? 1 : 0;
-        // MYRT_SCALAR_WREC: the wave-uniform step reads the FP64 record (no v_cvt_f64_f32)
-        if (!MYRT_SCALAR_WREC && r0 < P.compact_limit) {
-            const SCRec R = load_crec_scalar(P.crecs + r0);
-            return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
-        }
-#if MYRT_SCALAR_FULL
+        // the wave-uniform step reads the FP64 record (no v_cvt_f64_f32; C3/C5 -0.5 % against
+        // the compact record through SGPRs)
         const SRec R = load_rec_scalar(P.recs + r0);
-        if (MYRT_NEARSEL && FAST && soct >= 0)      // FP64 bounds in SGPRs: scalar selects
-            return inner_step_rec<COUNT, FAST, SHADOW, 2>(P, R, ref, o, inv, lim, st, c, soct);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
-#endif
     }
     if (COUNT && !P.count_ref) {             // redundancy of the per-lane loads below
         unsigned long long left = __ballot(1);
@@ -661,26 +508,7 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
         c.div_lanes += 1;
         c.div_distinct += ((int)(threadIdx.x & 63) == my_leader) ? 1 : 0;
     }
-    if (MYRT_LDS_TOP_CODE && ref < st.top_n) {   // near-root record: this wave's LDS copy
-        const lds_crec* q = st.top + 4 * ref;
-        const f32x4 a = q[0], b = q[1], e = q[2];
-        // the refs are read as integers: bit-casting elements of a float vector read every
-        // element as element 0 (the same miscompile as the SGPR-tuple case, load_crec_scalar)
-        const i32x4 f = *(const lds_i32x4*)(q + 3);
-        CRec R;
-        R.lo[0][0] = a.x; R.lo[0][1] = a.y; R.lo[0][2] = a.z; R.lo[1][0] = a.w;
-        R.lo[1][1] = b.x; R.lo[1][2] = b.y; R.hi[0][0] = b.z; R.hi[0][1] = b.w;
-        R.hi[0][2] = e.x; R.hi[1][0] = e.y; R.hi[1][1] = e.z; R.hi[1][2] = e.w;
-        R.ref[0] = f.x; R.ref[1] = f.y;
-        return inner_step_rec<COUNT, FAST, SHADOW, kLaneSel>(P, R, ref, o, inv, lim, st, c);
-    }
-    if (ref < P.compact_limit) {
-#if MYRT_CREC56
-        return inner_step_rec<COUNT, FAST, SHADOW, kLaneSel>(P, load_crec56(P.crecs + ref), ref, o, inv, lim, st, c);
-#else
-        return inner_step_rec<COUNT, FAST, SHADOW, kLaneSel>(P, P.crecs[ref], ref, o, inv, lim, st, c);
-#endif
-    }
+    if (ref < P.compact_limit) return inner_step_rec<COUNT, FAST, SHADOW>(P, P.crecs[ref], ref, o, inv, lim, st, c);
     return inner_step_rec<COUNT, FAST, SHADOW>(P, P.recs[ref], ref, o, inv, lim, st, c);
 }
 
@@ -709,10 +537,9 @@ __device__ __forceinline__ bool pop_next(const RenderParams& P, Stack& st, int b
 template <bool COUNT, bool FAST, bool SHADOW, class Leaf, class Limit>
 __device__ __forceinline__ bool walk(const RenderParams& P, int ref, const V3& o, const V3& inv, Stack& st, int base,
                                      Counts& c, Leaf leaf, Limit limit) {
-    const int soct = FAST ? wave_octant(inv) : -1;
     for (;;) {
         if (ref >= 0) {
-            if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, limit(), st, c, soct)) continue;
+            if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, limit(), st, c)) continue;
         } else {
             if (leaf(ref)) return true;
         }
@@ -892,12 +719,9 @@ __device__ __forceinline__ bool unified_leaf(const RenderParams& P, int ref, Sta
     return false;
 }
 
-#ifndef MYRT_ONE_TRI
-#define MYRT_ONE_TRI 0
-#endif
 template <bool COUNT, bool SHADOW, bool FAST>
 __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Stack& st, const V3& o, const V3& d,
-                                            const V3& inv, double tlo, double tmax, Hit& h, Counts& c, int soct = -1) {
+                                            const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
     if (COUNT && !P.count_ref) {             // divergence breakdown of this iteration
         const bool in = ref >= 0;
         const unsigned long long bi = __ballot(in), bl = __ballot(!in);
@@ -908,121 +732,12 @@ __device__ __forceinline__ int unified_step(const RenderParams& P, int& ref, Sta
         c.it_lane_leaf[SHADOW] += in ? 0 : 1;
     }
     if (ref >= 0) {
-        if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c,
-                                            soct))
+        if (inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c))
             return 0;
-    } else if (MYRT_ONE_TRI && ~ref < P.tlas_leaf_base) {
-        // one triangle per iteration: a lane in a 2-triangle leaf continues with the second
-        // triangle next iteration while the other lanes keep traversing, so an iteration
-        // pays for at most one record and one triangle
-        const int t = ~ref;
-        auto one = [&](const auto* tris) -> int {
-            const auto T = tris[t];          // by value: `last` arrives with the vertices
-            if (COUNT) c.tris++;
-            if (SHADOW) {
-                if (tri_shadow(T, o, d, 0.0, tmax, P.eps)) return 2;
-            } else {
-                tri_closest(T, o, d, tlo, P.eps, h, t, T.prim);
-            }
-            return T.last ? 1 : 0;
-        };
-        const int r = P.ctris ? one(P.ctris) : one(P.tris);
-        if (r == 2) return 2;
-        if (r == 0) { ref = ~(t + 1); return 0; }
-    } else {
-        if (unified_leaf<COUNT, SHADOW, FAST>(P, ref, st, o, d, inv, tlo, tmax, h, c)) return 2;
+    } else if (unified_leaf<COUNT, SHADOW, FAST>(P, ref, st, o, d, inv, tlo, tmax, h, c)) {
+        return 2;
     }
     return pop_next<COUNT, SHADOW>(P, st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref, c) ? 0 : 1;
-}
-
-#ifndef MYRT_WHILE_WHILE
-#define MYRT_WHILE_WHILE 0
-#endif
-// While-while form (Aila & Laine 2009): a lane descends through inner records until it sits
-// at a leaf, and leaves are processed only once every lane of the wave has left the inner
-// loop, so one wave iteration no longer pays for both the record and the triangle path.
-// Returns 1 = stack exhausted, 2 = occluded.  Visit order is unchanged.
-template <bool COUNT, bool SHADOW, bool FAST>
-__device__ __forceinline__ int unified_walk_ww(const RenderParams& P, int ref, Stack& st, const V3& o, const V3& d,
-                                               const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
-    for (;;) {
-        bool alive = true;
-        while (ref >= 0) {
-            if (COUNT) { if (SHADOW) c.it_shadow++; else c.it_closest++; }
-            const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
-            if (!inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, lim, st, c) &&
-                !pop_next<COUNT, SHADOW>(P, st, 0, lim, ref, c)) {
-                alive = false;
-                break;
-            }
-        }
-        if (!alive) return 1;
-        if (COUNT) { if (SHADOW) c.it_shadow++; else c.it_closest++; }
-        if (unified_leaf<COUNT, SHADOW, FAST>(P, ref, st, o, d, inv, tlo, tmax, h, c)) return 2;
-        if (!pop_next<COUNT, SHADOW>(P, st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref, c)) return 1;
-    }
-}
-
-// Postponed-leaf form of the unified walk.  With leaves handled where they are met, a wave
-// ran its leaf block with ~10 of its 64 lanes (C3 closest hit: 4.9M lane leaf runs in 0.47M
-// wave leaf blocks, rt_work_counters iter_*), and that block - one or two Moeller-Trumbore
-// tests with an FP64 division each - costs about as much as two inner steps.  Here a lane
-// that reaches a BLAS leaf run parks it (`pend`) and keeps traversing; the wave runs the
-// leaf block once P.leaf_batch lanes hold a leaf, or when no lane can step (each active lane
-// has parked a leaf and met a second one, or has exhausted its stack).
-// Exactness: a lane holds one leaf at a time, so it still tests its leaves in its visit
-// order (near first, ties to L); only the pruning limit lags (h.t is updated at the leaf
-// block), which visits more nodes - every one of which the reference visits, as it does not
-// prune - so the closest hit, including which of two equal-t hits wins, is the reference's
-// (RTContext.swift:544-610).  Any-hit walks are order-free and stop at the leaf block that
-// finds an occluder.  Returns true when occluded (any hit).
-#ifndef MYRT_PL
-#define MYRT_PL 0          // measured slower (DESIGN §4 lost experiments): compiled out by default
-#endif
-template <bool COUNT, bool SHADOW, bool FAST>
-__device__ __forceinline__ bool unified_walk_pl(const RenderParams& P, int ref, Stack& st, const V3& o, const V3& d,
-                                                const V3& inv, double tlo, double tmax, Hit& h, Counts& c) {
-    const int base = st.sp;
-    int pend = 0;           // parked BLAS leaf run (a leaf ref, < 0); 0 = none
-    bool live = true;       // `ref` holds a node still to process
-    bool occ = false;
-    for (;;) {
-        const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
-        if (COUNT) {
-            if (SHADOW) c.it_shadow++; else c.it_closest++;
-            const bool in = live && ref >= 0;
-            const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
-            c.it_wave_inner[SHADOW] += (first && __ballot(in)) ? 1 : 0;
-            c.it_lane_inner[SHADOW] += in ? 1 : 0;
-        }
-        if (live) {
-            bool pop = false;
-            if (ref >= 0) {
-                pop = !inner_step<COUNT, FAST, SHADOW>(P, ref, o, inv, lim, st, c);
-            } else if (~ref >= P.tlas_leaf_base) {                  // TLAS leaf: push the BLAS roots
-                unified_leaf<COUNT, SHADOW, FAST>(P, ref, st, o, d, inv, tlo, tmax, h, c);
-                pop = true;
-            } else if (pend == 0) {                                  // park the leaf, move on
-                pend = ref;
-                pop = true;
-            }                                                        // else: wait for the leaf block
-            if (pop) live = pop_next<COUNT, SHADOW>(P, st, base, lim, ref, c);
-        }
-        const bool stuck = !live || (ref < 0 && pend != 0 && ~ref < P.tlas_leaf_base);
-        const unsigned long long held = __ballot(pend != 0);
-        if (held && (__popcll(held) >= P.leaf_batch || __ballot(stuck) == __ballot(1))) {
-            if (COUNT) {
-                const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
-                c.it_wave_leaf[SHADOW] += first ? 1 : 0;
-                c.it_lane_leaf[SHADOW] += pend != 0 ? 1 : 0;
-            }
-            if (pend != 0) {
-                occ = unified_leaf<COUNT, SHADOW, FAST>(P, pend, st, o, d, inv, tlo, tmax, h, c);
-                pend = 0;
-            }
-        }
-        if (occ || (!live && pend == 0)) return occ;
-    }
 }
 
 // Root test of the unified walk (the TLAS root is popped and tested first,
@@ -1042,389 +757,16 @@ __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3
                                                  double tlo, Hit& h, Stack& st, Counts& c) {
     int ref;
     if (!unified_begin(P, o, inv, DINF, ref)) return;   // the stack is empty here (base 0)
-    if (MYRT_PL && !MYRT_REF(P) && P.leaf_batch > 0) {
-        unified_walk_pl<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c);
-        return;
-    }
-    if (MYRT_WHILE_WHILE) {
-        unified_walk_ww<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c);
-        return;
-    }
-    const int soct = FAST ? wave_octant(inv) : -1;
-    do { if (COUNT || MYRT_WAVE_TIMES) c.it_closest++; } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c, soct) == 0);
+    do {
+        if (COUNT || MYRT_WAVE_TIMES) c.it_closest++;
+    } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0);
 }
-// ------------------------------------------------------------ FP32-enclosed walks (MYRT_F32)
-// The reference's slab test is FP64 (hitAABB, RTContext.swift:557-565).  A wave64 FP32 op
-// issues in 2 cycles on gfx950 and an FP64 op in 4, and the FP64 test of a compact record
-// also needs 12 v_cvt_f64_f32.  For rays with no zero direction component these walks test
-// compact records in FP32 with a bound that encloses the FP64 values (slab32.h) and take a
-// decision in FP32 only when the enclosure makes it certain:
-//   * an uncertain hit/miss is recomputed in FP64 for that child, so every visited node is
-//     one the reference visits (pruning aside);
-//   * an uncertain near/far order is taken from the FP32 values and remembered: the order
-//     only decides which of two EQUAL-t triangle hits wins (H2; pruning never removes the
-//     closest hit's node), so a ray that took an uncertain order AND met an equal-t
-//     candidate is walked again in the exact FP64 order;
-//   * any-hit walks are unordered (MYRT_SHADOW_ORDER) and need only hit/miss.
-// Measured slower (C3 0.92 vs 0.79 ms/frame, C5 4.16 vs 3.45; not yet profiled, the extra
-// enclosure state per lane is the suspect), so they are compiled out by default: build with
-// -DMYRT_F32=1 to include them; RenderParams::use_f32 = 0 (host: MYRT_F32=0) then selects FP64.
-#ifndef MYRT_F32
-#define MYRT_F32 0
-#endif
-template <bool SHADOW, class Rec>
-__device__ __forceinline__ bool inner_step_f32(const RenderParams& P, const Rec& R, int& ref, const V3& o,
-                                               const V3& d, const f32slab::RayF& F, float lim_up, Stack& st,
-                                               bool& amb) {
-    float m0, lo0, hi0, m1, lo1, hi1;
-    int c0 = f32slab::test(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], F, P.eps_up32,
-                           P.eps_dn32, m0, lo0, hi0);
-    int c1 = f32slab::test(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], F, P.eps_up32,
-                           P.eps_dn32, m1, lo1, hi1);
-    if (c0 < 0 || c1 < 0) {                 // rare: the reference's FP64 test for that child
-        const V3 inv = rcp(d);
-        double t;
-        if (c0 < 0) {
-            c0 = slab_hit<true>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
-                                P.eps, t) ? 1 : 0;
-            f32slab::enclose(t, m0, lo0, hi0);
-        }
-        if (c1 < 0) {
-            c1 = slab_hit<true>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
-                                P.eps, t) ? 1 : 0;
-            f32slab::enclose(t, m1, lo1, hi1);
-        }
-    }
-    const bool h0 = c0 > 0 && !(lo0 > lim_up);     // lo <= FP64 tmin: prunes only what FP64 would
-    const bool h1 = c1 > 0 && !(lo1 > lim_up);
-    const int a = R.ref[0], b = R.ref[1];
-    const bool both = h0 && h1;
-    bool sw = false;
-    if (!SHADOW) {
-        const bool yes = lo0 > hi1, no = hi0 <= lo1;  // certainly t0 > t1 / certainly not
-        sw = yes || (!no && m0 > m1);
-        amb = amb || (both && !yes && !no);
-    }
-    st.push_if(both, sw ? a : b, (double)(sw ? lo0 : lo1));
-    ref = both ? (sw ? b : a) : (h0 ? a : b);
-    return h0 || h1;
-}
-template <bool SHADOW>
-__device__ __forceinline__ bool inner_step_f32_any(const RenderParams& P, int& ref, const V3& o, const V3& d,
-                                                   const f32slab::RayF& F, float lim_up, Stack& st, bool& amb) {
-    const int r0 = __builtin_amdgcn_readfirstlane(ref);
-    if (P.scalar_nodes && __all(ref == r0))
-        return inner_step_f32<SHADOW>(P, load_crec_scalar(P.crecs + r0), ref, o, d, F, lim_up, st, amb);
-    return inner_step_f32<SHADOW>(P, P.crecs[ref], ref, o, d, F, lim_up, st, amb);
-}
-// tri_closest that also reports an equal-t candidate
-template <class Tri>
-__device__ __forceinline__ void tri_closest_tie(const Tri& T, const V3& o_mb, const V3& d, double tlo, double eps,
-                                                Hit& h, int triIdx, int instIdx, bool& tie) {
-    V3 v0, e1, e2;
-    tri_geom(T, v0, e1, e2);
-    const V3 pvec = cross(d, e2);
-    const double det = dot(e1, pvec);
-    if (fabs(det) < eps) return;
-    const double invDet = 1.0 / det;
-    const V3 tvec = o_mb - v0;
-    const double u = dot(tvec, pvec) * invDet;
-    if (u < 0.0 || u > 1.0) return;
-    const V3 q = cross(tvec, e1);
-    const double v = dot(d, q) * invDet;
-    if (v < 0.0 || u + v > 1.0) return;
-    const double t = dot(e2, q) * invDet;
-    if (t <= smax(eps, tlo)) return;
-    if (t >= h.t) { tie = tie || (t == h.t); return; }
-    h.t = t; h.u = u; h.v = v; h.tri = triIdx; h.inst = instIdx;
-}
-template <bool SHADOW>
-__device__ __forceinline__ int unified_step_f32(const RenderParams& P, int& ref, Stack& st, const V3& o, const V3& d,
-                                                const f32slab::RayF& F, double tlo, double tmax, Hit& h, bool& amb,
-                                                bool& tie, float& lim32, Counts& c) {
-    if (ref >= 0) {
-        if (ref < P.compact_limit) {
-            if (inner_step_f32_any<SHADOW>(P, ref, o, d, F, lim32, st, amb)) return 0;
-        } else if (inner_step<false, true, SHADOW>(P, ref, o, rcp(d),
-                                                   (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, st, c)) {
-            return 0;                                 // full FP64 records (TLAS): the exact step
-        }
-    } else {
-        const int e = ~ref;
-        if (e < P.tlas_leaf_base) {                   // BLAS leaf run
-            auto run = [&](const auto* tris) -> bool {
-                for (int t = e;; ++t) {
-                    const auto T = tris[t];
-                    if (SHADOW) {
-                        if (tri_shadow(T, o, d, 0.0, tmax, P.eps)) return true;
-                    } else {
-                        tri_closest_tie(T, o, d, tlo, P.eps, h, t, T.prim, tie);
-                    }
-                    if (T.last) break;
-                }
-                return false;
-            };
-            if (P.ctris ? run(P.ctris) : run(P.tris)) return 2;
-            if (!SHADOW) lim32 = f32slab::up(h.t * P.prune_rel + P.prune_abs);
-        } else if (unified_leaf<false, SHADOW, true>(P, ref, st, o, d, rcp(d), tlo, tmax, h, c)) {
-            return 2;                                 // TLAS leaf: instance roots in FP64
-        }
-    }
-    return pop_next<false, SHADOW>(P, st, 0, (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs, ref, c) ? 0 : 1;
-}
-__device__ __forceinline__ void uni_closest_f32(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
-                                                double tlo, Hit& h, Stack& st, Counts& c) {
-    int ref;
-    if (!unified_begin(P, o, inv, DINF, ref)) return;
-    const f32slab::RayF F = f32slab::make(o.x, o.y, o.z, inv.x, inv.y, inv.z, P.bmax32);
-    bool amb = false, tie = false;
-    float lim32 = __builtin_inff();
-    while (unified_step_f32<false>(P, ref, st, o, d, F, tlo, DINF, h, amb, tie, lim32, c) == 0) {}
-    if (amb && tie) {                               // equal-t hits after an uncertain order
-        h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-        st.reset(0);
-        uni_closest_walk<false, true>(P, o, d, rcp(d), tlo, h, st, c);
-    }
-}
-__device__ __forceinline__ bool uni_occluded_f32(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
-                                                 double tmax, Stack& st, Counts& c) {
-    int ref;
-    if (!unified_begin(P, o, inv, tmax * P.prune_rel + P.prune_abs, ref)) return false;
-    const f32slab::RayF F = f32slab::make(o.x, o.y, o.z, inv.x, inv.y, inv.z, P.bmax32);
-    Hit h;                                           // unused by any-hit steps
-    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-    bool amb = false, tie = false;
-    float lim32 = f32slab::up(tmax * P.prune_rel + P.prune_abs);
-    const int base = st.sp;
-    int r;
-    while ((r = unified_step_f32<true>(P, ref, st, o, d, F, 0.0, tmax, h, amb, tie, lim32, c)) == 0) {}
-    st.reset(base);
-    return r == 2;
-}
-
-// ------------------------------------------------------------------ packet walks (MYRT_PACKET)
-// Identity scenes, wave-coherent rays (primary rays of an 8x8 tile, their shadow rays): the
-// whole wave walks ONE node sequence, the union of what its lanes need.  Each step's record
-// or triangle is wave-uniform, so it arrives through the scalar cache (no per-lane vector
-// loads) and the control flow never splits into an inner-node and a leaf branch; a lane
-// takes part in a step when the node is in its mask (its box test hit, within its own
-// pruning limit).
-//   * Stack: {ref, lane mask} entries in the wave's LDS stack slab (the per-lane stack is
-//     empty while a packet walk runs; 512 entries, the host bound is kStackCap).
-//   * Closest hit: at a node where lanes want both children the wave takes the majority's
-//     near child first.  A lane whose own near-first order (RTContext.swift:600-606) differs
-//     is flagged; the order only decides which of two EQUAL-t hits wins (H2; pruned subtrees
-//     cannot hold the final hit, H3), so a flagged lane that also met an equal-t candidate
-//     is walked again alone in the reference order (uni_closest_walk).  Every other lane's
-//     result is the reference's.
-//   * Any hit: order-free; a lane leaves the packet at its first occluder.
-#ifndef MYRT_PACKET
-#define MYRT_PACKET 0      // measured slower (DESIGN §4 lost experiments): compiled out by default
-#endif
-typedef const __attribute__((address_space(4))) WRec c4_wrec;
-typedef const __attribute__((address_space(4))) TriRec c4_tri;
-typedef const __attribute__((address_space(4))) DInstance c4_inst;
-typedef const __attribute__((address_space(4))) DTlasLeafEntry c4_leaf;
-__device__ __forceinline__ int wuni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ unsigned long long wuni64(unsigned long long x) {
-    return (unsigned long long)(unsigned)wuni((int)(unsigned)x) |
-           ((unsigned long long)(unsigned)wuni((int)(unsigned)(x >> 32)) << 32);
-}
-// wave-uniform stack entry k = {ref, mask} at slab[2k], slab[2k + 1]; one lane stores it
-__device__ __forceinline__ void wpush(lds_u64* slab, int& sp, int ref, unsigned long long mask) {
-    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
-        slab[2 * sp] = (unsigned long long)(unsigned)ref;
-        slab[2 * sp + 1] = mask;
-    }
-    ++sp;
-}
-__device__ __forceinline__ void wpop(lds_u64* slab, int& sp, int& ref, unsigned long long& mask) {
-    --sp;
-    ref = wuni((int)(unsigned)slab[2 * sp]);
-    mask = wuni64(slab[2 * sp + 1]);
-}
-__device__ __forceinline__ bool lane_in(unsigned long long m) { return (m >> (threadIdx.x & 63)) & 1ull; }
-// wave-uniform records read through the constant address space: scalar (s_load) loads
-__device__ __forceinline__ WRec load_wrec_uniform(const WRec* g) {
-    c4_wrec* p = (c4_wrec*)g;
-    WRec R;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { R.lo[c][k] = p->lo[c][k]; R.hi[c][k] = p->hi[c][k]; }
-        R.ref[c] = p->ref[c];
-    }
-    return R;
-}
-__device__ __forceinline__ TriRec load_tri_uniform(const TriRec* g) {
-    c4_tri* p = (c4_tri*)g;
-    TriRec T;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { T.v0[k] = p->v0[k]; T.e1[k] = p->e1[k]; T.e2[k] = p->e2[k]; }
-    T.last = p->last;
-    T.prim = p->prim;
-    return T;
-}
-
-// Closest hit, every lane's 1/d finite (FAST slabs).  Returns true when this lane must be
-// walked again in the reference order (order deviation + equal-t candidate).
-__device__ __forceinline__ bool uni_closest_packet(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
-                                                   double tlo, Hit& h, Stack& st) {
-    lds_u64* slab = st.lds - (threadIdx.x & 63);
-    double d0;
-    unsigned long long m = __ballot(slab_hit<true>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2],
-                                                   P.tlas_root_hi[0], P.tlas_root_hi[1], P.tlas_root_hi[2], o, inv,
-                                                   P.eps, d0));
-    if (!m) return false;
-    int ref = P.tlas_root_ref, sp = 0;
-    bool dev = false, tie = false;
-    for (;;) {
-        const bool in = lane_in(m);
-        if (ref >= 0) {
-            const WRec R = load_wrec_uniform(P.recs + ref);
-            double t0 = 0, t1 = 0;
-            bool h0 = false, h1 = false;
-            if (in) {
-                const double lim = h.t * P.prune_rel + P.prune_abs;
-                h0 = slab_hit<true>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
-                                    P.eps, t0) && !(t0 > lim);
-                h1 = slab_hit<true>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
-                                    P.eps, t1) && !(t1 > lim);
-            }
-            const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
-            if (m0 && m1) {
-                const bool both = h0 && h1, sw = both && (t0 > t1);
-                const bool wswap = 2 * __popcll(__ballot(sw)) > __popcll(__ballot(both));
-                dev = dev || (both && sw != wswap);
-                wpush(slab, sp, wswap ? R.ref[0] : R.ref[1], wswap ? m0 : m1);
-                ref = wswap ? R.ref[1] : R.ref[0];
-                m = wswap ? m1 : m0;
-                continue;
-            }
-            if (m0 | m1) {
-                ref = m0 ? R.ref[0] : R.ref[1];
-                m = m0 | m1;
-                continue;
-            }
-        } else {
-            const int e = ~ref;
-            if (e < P.tlas_leaf_base) {                          // BLAS leaf run, in leaf order
-                for (int t = e;; ++t) {
-                    const TriRec T = load_tri_uniform(P.tris + t);
-                    if (in) tri_closest_tie(T, o, d, tlo, P.eps, h, t, T.prim, tie);
-                    if (T.last) break;
-                }
-            } else {                                             // TLAS leaf: roots pushed in reverse
-                const int k0 = e - P.tlas_leaf_base;
-                int k1 = k0;
-                while (!((c4_leaf*)P.tlas_leaf)[k1].last) ++k1;
-                for (int k = k1; k >= k0; --k) {
-                    const c4_inst& I = ((c4_inst*)P.insts)[((c4_leaf*)P.tlas_leaf)[k].inst];
-                    double dr;
-                    bool hb = false;
-                    if (in) hb = slab_hit<true>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
-                                                I.root_hi[2], o, inv, P.eps, dr) &&
-                                 !(dr > h.t * P.prune_rel + P.prune_abs);
-                    const unsigned long long mk = __ballot(hb);
-                    if (mk) wpush(slab, sp, I.root_ref, mk);
-                }
-            }
-        }
-        if (sp == 0) break;
-        wpop(slab, sp, ref, m);
-    }
-    return dev && tie;
-}
-
-// Any hit; `live` = this lane has a shadow ray.  Returns the lane's occlusion.
-__device__ __forceinline__ bool uni_occluded_packet(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
-                                                    double tmax, Stack& st) {
-    lds_u64* slab = st.lds - (threadIdx.x & 63);
-    const double lim = tmax * P.prune_rel + P.prune_abs;
-    double d0;
-    unsigned long long alive = __ballot(slab_hit<true>(P.tlas_root_lo[0], P.tlas_root_lo[1], P.tlas_root_lo[2],
-                                                       P.tlas_root_hi[0], P.tlas_root_hi[1], P.tlas_root_hi[2], o,
-                                                       inv, P.eps, d0) && !(d0 > lim));
-    const unsigned long long entered = alive;
-    int ref = P.tlas_root_ref, sp = 0;
-    unsigned long long m = alive;
-    for (;;) {
-        const bool in = lane_in(m);
-        if (ref >= 0) {
-            const WRec R = load_wrec_uniform(P.recs + ref);
-            double t0, t1;
-            bool h0 = false, h1 = false;
-            if (in) {
-                h0 = slab_hit<true>(R.lo[0][0], R.lo[0][1], R.lo[0][2], R.hi[0][0], R.hi[0][1], R.hi[0][2], o, inv,
-                                    P.eps, t0) && !(t0 > lim);
-                h1 = slab_hit<true>(R.lo[1][0], R.lo[1][1], R.lo[1][2], R.hi[1][0], R.hi[1][1], R.hi[1][2], o, inv,
-                                    P.eps, t1) && !(t1 > lim);
-            }
-            const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
-            if (m0 && m1) {                                      // L first (any-hit order is free)
-                wpush(slab, sp, R.ref[1], m1);
-                ref = R.ref[0];
-                m = m0;
-                continue;
-            }
-            if (m0 | m1) {
-                ref = m0 ? R.ref[0] : R.ref[1];
-                m = m0 | m1;
-                continue;
-            }
-        } else {
-            const int e = ~ref;
-            if (e < P.tlas_leaf_base) {
-                bool occ = false;
-                for (int t = e;; ++t) {
-                    const TriRec T = load_tri_uniform(P.tris + t);
-                    if (in && !occ) occ = tri_shadow(T, o, d, 0.0, tmax, P.eps);
-                    if (T.last) break;
-                }
-                alive &= ~__ballot(occ);
-                if (!alive) break;
-            } else {
-                const int k0 = e - P.tlas_leaf_base;
-                int k1 = k0;
-                while (!((c4_leaf*)P.tlas_leaf)[k1].last) ++k1;
-                for (int k = k1; k >= k0; --k) {
-                    const c4_inst& I = ((c4_inst*)P.insts)[((c4_leaf*)P.tlas_leaf)[k].inst];
-                    double dr;
-                    bool hb = false;
-                    if (in) hb = slab_hit<true>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1],
-                                                I.root_hi[2], o, inv, P.eps, dr) && !(dr > lim);
-                    const unsigned long long mk = __ballot(hb);
-                    if (mk) wpush(slab, sp, I.root_ref, mk);
-                }
-            }
-        }
-        for (;;) {                                               // pop an entry with live lanes
-            if (sp == 0) return lane_in(entered & ~alive);
-            wpop(slab, sp, ref, m);
-            m &= alive;
-            if (m) break;
-        }
-    }
-    return lane_in(entered & ~alive);
-}
-
 template <bool COUNT>
 __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
                                             double tlo, Hit& h, Stack& st, Counts& c) {
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-    if (__all(finite3(inv))) {
-        if (MYRT_PACKET && !COUNT && (P.packet & 1)) {
-            if (uni_closest_packet(P, o, d, inv, tlo, h, st)) {      // rare: reference order again
-                h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-                uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
-            }
-            return;
-        }
-        if (MYRT_F32 && !COUNT && P.use_f32) uni_closest_f32(P, o, d, inv, tlo, h, st, c);
-        else uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
-    } else {
-        uni_closest_walk<COUNT, false>(P, o, d, inv, tlo, h, st, c);
-    }
+    if (__all(finite3(inv))) uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
+    else uni_closest_walk<COUNT, false>(P, o, d, inv, tlo, h, st, c);
 }
 template <bool COUNT, bool FAST>
 __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
@@ -1435,14 +777,9 @@ __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     const int base = st.sp;
     int r;
-    if (MYRT_PL && !MYRT_REF(P) && P.leaf_batch > 0) {
-        r = unified_walk_pl<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c) ? 2 : 1;
-    } else if (MYRT_WHILE_WHILE) {
-        r = unified_walk_ww<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c);
-    } else {
-        const int soct = FAST ? wave_octant(inv) : -1;
-        do { if (COUNT || MYRT_WAVE_TIMES) c.it_shadow++; } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c, soct)) == 0);
-    }
+    do {
+        if (COUNT || MYRT_WAVE_TIMES) c.it_shadow++;
+    } while ((r = unified_step<COUNT, true, FAST>(P, ref, st, o, d, inv, 0.0, tmax, h, c)) == 0);
     st.reset(base);
     return r == 2;
 }
@@ -1451,11 +788,7 @@ __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o,
                                              Stack& st, Counts& c) {
     if (!P.has_tlas) return false;
     const V3 inv = rcp(d);
-    if (__all(finite3(inv))) {
-        if (MYRT_PACKET && !COUNT && (P.packet & 2)) return uni_occluded_packet(P, o, d, inv, tmax, st);
-        if (MYRT_F32 && !COUNT && P.use_f32) return uni_occluded_f32(P, o, d, inv, tmax, st, c);
-        return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
-    }
+    if (__all(finite3(inv))) return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
     return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);
 }
 

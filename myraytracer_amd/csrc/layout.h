@@ -93,6 +93,21 @@ constexpr int kJitterCells = 100;    // buildStratifiedJitter 10x10 table (Objec
 
 struct DTlasLeafEntry { int32_t inst; int32_t last; };
 
+// A queued mirror/conductor bounce ray (compacted bounce render, render.hip k_bounce): the
+// child trace(depth + 1) of one sample plus what its parent level adds back,
+// Lo_parent + M_parent * trace(depth + 1) (Object+Extension.swift:189-206, 252-275).
+// Level-k records live at [(k - 1) * cap, k * cap) of RenderParams::bounce.
+struct alignas(128) BounceRec {
+    double o[3], d[3];        // the reflected ray (origin p + N * shadowRayEpsilon, tMin 0)
+    double Lo[3], M[3];       // the parent level's radiance and its mirror/Fresnel multiplier
+    unsigned long long rng;   // the sample's PCG32 state after the parent's draws (roughness)
+    double time;              // the sample's ray time (instance motion)
+    int32_t i, j;             // pixel
+    int32_t parent;           // record of the parent level (global index), -1 = the primary sample
+    int32_t pad;
+};
+static_assert(sizeof(BounceRec) == 128, "BounceRec is one 128-B line");
+
 // Camera + frame constants precomputed on the host (Object+Extension.swift:58-93)
 struct DCamera {
     double eye[3], u[3], v[3], w[3];
@@ -122,9 +137,6 @@ struct RenderParams {
     DCamera cam;
     double eps, shadow_eps;
     double prune_rel, prune_abs;     // conservative t-pruning margins (DESIGN.md "H3")
-    float eps_up32, eps_dn32;        // eps rounded out to floats (slab32.h)
-    float bmax32;                    // >= every |coordinate| of the scene (slab32.h overflow guard)
-    int32_t use_f32;                 // FP32-enclosed slab walks (device.h MYRT_F32; host MYRT_F32=0 disables)
     double background[3], ambient[3];
     int32_t max_depth;
     int32_t chunk_first, chunk_step, num_chunks;   // selected 8-row chunks
@@ -135,15 +147,10 @@ struct RenderParams {
     int32_t stack_depth;             // LDS stack entries per lane
     int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
-    int32_t scalar_nodes;            // wave-uniform records via scalar loads (device.h inner_step)
     int32_t compact_limit;           // records below this index are read from crecs
     int32_t rot_slots;               // megakernel dispatch order: selected chunk rows rotated by this many
-    int32_t lds_top_n;               // megakernel: compact records [0, n) served from LDS (0 = off)
-    int32_t packet;                  // identity scenes: wave packet walks (device.h MYRT_PACKET)
     int32_t fast_rcp;                // every Moeller-Trumbore |det| >= eps lies in [2^-700, 2^1000]
                                      // (host bound): 1/det by device.h rcp_rn, bit-identical
-    int32_t leaf_batch;              // identity scenes: postponed-leaf walks run the leaf block once this
-                                     // many lanes hold a leaf (device.h unified_walk_pl; 0 = immediate leaves)
     const DAreaLight* alights;
     const double* jitter;            // [0..99] jitterX, [100..199] jitterY
     const long long* jstart;         // area lights: per-pixel first jitterIndex (packed rows)
@@ -155,6 +162,10 @@ struct RenderParams {
     // a launch covers selected chunks [slot_base, slot_base + gridDim.x / tiles-per-chunk)
     void* deep;
     int32_t slot_base;
+    // compacted bounce render (render.hip k_bounce): queued bounce rays, `bounce_cap` records per
+    // level; nullptr = the bounce megakernel
+    BounceRec* bounce;
+    int64_t bounce_cap;
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
     unsigned long long* counters;    // [0] shadow rays cast, [1] secondary rays, [2..12] work counters,
@@ -163,7 +174,12 @@ struct RenderParams {
     unsigned long long* wave_times;  // debug (rt_debug_wave_times): per wave {start, end, tile} in 100 MHz ticks
 };
 
-constexpr int kCounterWords = 32;   // u64 words behind RenderParams::counters
+constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters
+// Compacted bounce render: words [32, 64) of the counters.  Level k (1..kMaxQueueLevels) has its
+// queue length at kQueueCount + k and its work-grab cursor at kQueueGrab + k; word kQueueDone
+// counts the last level's finished waves (the last one zeroes the queue words for the next launch).
+constexpr int kQueueDone = 32, kQueueCount = 32, kQueueGrab = 48;
+constexpr int kMaxQueueLevels = 15;
 constexpr int kCounterShadowTraced = 13;
 constexpr int kMaxDepthGPU = 16;     // trace() levels kept in private memory per lane (deeper: RenderParams::deep)
 constexpr int64_t kDeepBytesCap = 8ll << 30;   // device bytes of deep frames per launch batch
@@ -172,13 +188,5 @@ constexpr int64_t kDeepBytesCap = 8ll << 30;   // device bytes of deep frames pe
 // The reference gives the TLAS walk and each BLAS walk their own 64-entry stacks
 // (RTContext.swift:550, 623); one shared stack of 128 holds both at their limits.
 constexpr int kStackCap = 128;
-
-// Breadth-first record prefix of the first BLAS that the render kernels copy into LDS at
-// wave start (device.h Stack::top): the near-root levels every ray walks.
-constexpr int kLdsTopMax = 127;
-
-// Postponed-leaf walks (device.h unified_walk_pl): lanes holding a leaf before the wave runs
-// its leaf block (RenderParams::leaf_batch; host switch MYRT_LEAF_BATCH).
-constexpr int kLeafBatchDefault = 0;    // MYRT_PL builds only; measured slower at every batch size
 
 }  // namespace myrt

@@ -33,14 +33,143 @@
 
 namespace myrt {
 namespace dev {
+// Per-pixel PCG32 seed (Object+Extension.swift:294, SURVEY H7)
+__device__ __forceinline__ unsigned long long pixel_seed(int i, int j) {
+    return (((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull;
+}
+
+// Point lights at a hit (Object+Extension.swift:116-143): adds the unoccluded Blinn-Phong
+// terms to Lo.  With !(N.L > 0) the reference discards the occlusion result, so that walk is
+// skipped; the ray is still counted as cast.
+// park/unpark: the caller's PCG32 state moves to LDS around each walk (trace_path BOUNCE).
+template <bool COUNT, bool UNI, class Park, class Unpark>
+__device__ __forceinline__ void point_lights(const RenderParams& P, const DMaterial& M, const V3& N, const V3& p,
+                                             const V3& d, double time, Stack& st, Counts& c, V3& Lo, Park park,
+                                             Unpark unpark) {
+    for (int li = 0; li < P.num_plights; ++li) {
+        const DPointLight& PL = P.plights[li];
+        V3 wi = ld3(PL.position) - p;
+        const double dist = length(wi);
+        wi = normalize(wi);
+        const V3 so = p + wi * P.shadow_eps;
+        c.shadow++;
+        // The contribution is formed before the shadow walk (same expressions, same
+        // values) so that only it - not N, wi, view, material - stays live across the walk.
+        const double NdotL = smax(0.0, dot(N, wi));
+        V3 contrib = v3(0, 0, 0);
+        if (NdotL > 0) {
+            const double shininess = smax(1.0, M.phong);
+            const V3 Ld = ld3(M.diffuse) * NdotL;
+            const V3 view = normalize(-d);
+            const V3 hv = normalize(wi + view);
+            const double NdotH = smax(0.0, dot(N, hv));
+            const V3 Ls = ld3(M.specular) * phong_pow(NdotH, shininess);
+            const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
+            contrib = (Ld + Ls) * atten;
+        }
+        // pin it here: otherwise the compiler sinks the whole computation below the
+        // walk, into the one branch that uses it, and spills its inputs across the walk
+        asm volatile("" : "+v"(contrib.x), "+v"(contrib.y), "+v"(contrib.z));
+        if (NdotL > 0 || MYRT_REF(P)) {
+            c.shadow_traced++;
+            park();
+            const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
+                                     : occluded<COUNT>(P, so, wi, dist, time, st, c);
+            unpark();
+            if (!blocked && NdotL > 0) Lo = Lo + contrib;
+        }
+    }
+}
+
+// ---- compacted bounce render (mirror/conductor scenes, one traced sample per pixel) --------
+// The primary pass renders every pixel's primary ray and shadow rays in the spill-free
+// primary instantiation; a lane whose hit is a mirror or conductor below maxRecursionDepth
+// appends its reflected ray to the level-1 queue instead of tracing it (wave ballot + popc
+// prefix, one atomic per wave).  k_bounce traces one level's queue, appending the next level;
+// a ray that ends resolves its sample backward through its ancestors' records with the
+// per-level NaN guard, Lo_k + M_k * L_(k+1) (Object+Extension.swift:189-206, 252-283), and
+// stores the pixel.  Same operations on the same values as the recursion: identical frames.
+
+// Queue slots for the lanes of this wave that `want` a ray at `level`: returns the record's
+// global index, or -1.
+__device__ __forceinline__ long long queue_reserve(const RenderParams& P, int level, bool want) {
+    const unsigned long long m = __ballot(want);
+    if (m == 0) return -1;
+    const int leader = __builtin_ctzll(m);
+    unsigned base = 0;
+    if ((int)(threadIdx.x & 63) == leader)
+        base = (unsigned)atomicAdd(&P.counters[kQueueCount + level], (unsigned long long)__popcll(m));
+    base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
+    const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    return want ? (long long)(level - 1) * P.bounce_cap + (long long)(base + below) : -1ll;
+}
+
+// The reflected ray of a mirror/conductor hit and its multiplier (Object+Extension.swift:
+// 189-206, 252-275) into record q; the parent's Lo follows after its shadow walks.
+__device__ __forceinline__ void queue_write(const RenderParams& P, long long q, const DMaterial& M, const V3& d,
+                                            const V3& N, const V3& p, PCG32& rng, double time, int i, int j,
+                                            int parent) {
+    V3 mult;
+    if (M.type == RT_MAT_MIRROR) {
+        mult = ld3(M.mirror);
+    } else {
+        const double cosI = smax(0.0, -dot(d, N));
+        mult = fresnel_conductor(M.ior, M.absorption_index, cosI) * ld3(M.mirror);
+    }
+    V3 rd = normalize(reflect(d, N));
+    if (M.roughness != 0.0) {
+        V3 t, b;
+        onb(rd, t, b);
+        const double r1 = rng.nextFloat() - 0.5;
+        const double r2 = rng.nextFloat() - 0.5;
+        rd = (rd + (M.roughness * r1) * b) + (M.roughness * r2) * t;
+        rd = normalize(rd);
+    }
+    const V3 o = p + N * P.shadow_eps;
+    BounceRec& R = P.bounce[q];
+    R.o[0] = o.x; R.o[1] = o.y; R.o[2] = o.z;
+    R.d[0] = rd.x; R.d[1] = rd.y; R.d[2] = rd.z;
+    R.M[0] = mult.x; R.M[1] = mult.y; R.M[2] = mult.z;
+    R.rng = rng.state;
+    R.time = time;
+    R.i = i; R.j = j;
+    R.parent = parent;
+}
+__device__ __forceinline__ void queue_write_lo(const RenderParams& P, long long q, const V3& Lo) {
+    BounceRec& R = P.bounce[q];
+    R.Lo[0] = Lo.x; R.Lo[1] = Lo.y; R.Lo[2] = Lo.z;
+}
+
+// The pixel of one traced sample (RayTracer.swift:186-195 for RGBA8): px = (0 + col) / spp.
+__device__ __forceinline__ void store_pixel(const RenderParams& P, int i, int j, const V3& px) {
+    const size_t o = out_row_of(P, j >> 3, j & 7) * (size_t)P.cam.width + i;
+    if (P.out_rgb) {
+        P.out_rgb[o * 3 + 0] = px.x;
+        P.out_rgb[o * 3 + 1] = px.y;
+        P.out_rgb[o * 3 + 2] = px.z;
+    }
+    if (P.out_rgba8) {
+        const double cx = fmin(fmax(px.x, 0.0), 255.0), cy = fmin(fmax(px.y, 0.0), 255.0),
+                     cz = fmin(fmax(px.z, 0.0), 255.0);
+        const unsigned packed = (unsigned)(unsigned char)cx | ((unsigned)(unsigned char)cy << 8) |
+                                ((unsigned)(unsigned char)cz << 16) | (255u << 24);
+        reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
+    }
+}
+
 // trace() (Object+Extension.swift:96-283) for diffuse/mirror/conductor materials and
 // point lights.  The recursion Lo + M*trace(depth+1) is run forward and combined
 // backward with the same per-level NaN guard, so the result is the recursive one.
 // `rng_slot`: this lane's LDS slot for the PCG32 state (BOUNCE: the state waits there while
 // the rays are traced instead of being live - spilled - across the walks; nullptr = keep it)
-template <bool COUNT, bool BOUNCE, bool UNI>
+// QUEUE (primary pass of the compacted bounce render, !BOUNCE): a mirror/conductor hit queues
+// its reflected ray (level 1) and sets `deferred`; k_bounce delivers that pixel.  The PCG32
+// state is then read from rng_slot (the caller parks it there) and (i, j) give its stream.
+template <bool COUNT, bool BOUNCE, bool UNI, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
-                         Counts& c, __attribute__((address_space(3))) double* rng_slot) {
+                         Counts& c, __attribute__((address_space(3))) double* rng_slot, int i = 0, int j = 0,
+                         bool* deferred = nullptr) {
+    static_assert(!(QUEUE && BOUNCE), "the queued primary pass has no bounce loop");
     auto park = [&]() { if (BOUNCE && rng_slot) *rng_slot = __builtin_bit_cast(double, rng.state); };
     auto unpark = [&]() {
         if (BOUNCE && rng_slot) {
@@ -71,42 +200,22 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         const V3 N = frontFacing ? Ngeo : -Ngeo;
         const bool computeDirect = !(M.ior > 0) || frontFacing;
         V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
-        if (computeDirect) {
-            for (int li = 0; li < P.num_plights; ++li) {
-                const DPointLight& PL = P.plights[li];
-                V3 wi = ld3(PL.position) - p;
-                const double dist = length(wi);
-                wi = normalize(wi);
-                const V3 so = p + wi * P.shadow_eps;
-                c.shadow++;
-                // The contribution is formed before the shadow walk (same expressions, same
-                // values) so that only it - not N, wi, view, material - stays live across
-                // the walk.  With !(NdotL > 0) the reference discards the occlusion result
-                // (:126-141), so the walk is skipped; the ray is still counted as cast.
-                const double NdotL = smax(0.0, dot(N, wi));
-                V3 contrib = v3(0, 0, 0);
-                if (NdotL > 0) {
-                    const double shininess = smax(1.0, M.phong);
-                    const V3 Ld = ld3(M.diffuse) * NdotL;
-                    const V3 view = normalize(-d);
-                    const V3 hv = normalize(wi + view);
-                    const double NdotH = smax(0.0, dot(N, hv));
-                    const V3 Ls = ld3(M.specular) * phong_pow(NdotH, shininess);
-                    const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
-                    contrib = (Ld + Ls) * atten;
-                }
-                // pin it here: otherwise the compiler sinks the whole computation below the
-                // walk, into the one branch that uses it, and spills its inputs across the walk
-                asm volatile("" : "+v"(contrib.x), "+v"(contrib.y), "+v"(contrib.z));
-                if (NdotL > 0 || MYRT_REF(P)) {
-                    c.shadow_traced++;
-                    park();
-                    const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
-                                             : occluded<COUNT>(P, so, wi, dist, time, st, c);
-                    unpark();
-                    if (!blocked && NdotL > 0) Lo = Lo + contrib;
-                }
+        long long q = -1;
+        if (QUEUE) {     // the bounce ray is formed before the shadow walks: only q stays live
+            const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && P.max_depth > 0;
+            q = queue_reserve(P, 1, want);
+            if (q >= 0) {
+                PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*rng_slot), pixel_seed(i, j));
+                queue_write(P, q, M, d, N, p, r, time, i, j, -1);
+                c.secondary++;
             }
+        }
+        if (computeDirect) point_lights<COUNT, UNI>(P, M, N, p, d, time, st, c, Lo, park, unpark);
+        if (QUEUE && q >= 0) {
+            queue_write_lo(P, q, Lo);
+            *deferred = true;
+            L = v3(0, 0, 0);
+            break;
         }
         if (BOUNCE && (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && depth < P.max_depth &&
             depth < kMaxDepthGPU) {
@@ -154,10 +263,6 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 #ifndef MYRT_PIXLDS
 #define MYRT_PIXLDS 1        // pixel sum + PCG32 state kept in LDS across the walks (not spilled)
 #endif
-// Per-pixel PCG32 seed (Object+Extension.swift:294, SURVEY H7)
-__device__ __forceinline__ unsigned long long pixel_seed(int i, int j) {
-    return (((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull;
-}
 constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;
 #ifndef MYRT_TILE_W
 #define MYRT_TILE_W 8        // megakernel tile width in pixels (8: 8x8 tiles; 16: 16x4; 32: 32x2)
@@ -182,8 +287,11 @@ typedef __attribute__((address_space(3))) double lds_f64;
 namespace myrt {
 namespace dev {
 // UNI: identity scenes walk TLAS + BLAS as one tree (device.h unified_step).
-template <bool COUNT, bool BOUNCE, bool UNI>
+// QUEUE: primary pass of the compacted bounce render (one traced sample per pixel, host-checked):
+// mirror/conductor hits queue their reflected rays and their pixels are stored by k_bounce.
+template <bool COUNT, bool BOUNCE, bool UNI, bool QUEUE = false>
 __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams P) {
+    static_assert(!QUEUE || MYRT_PIXLDS, "the queued primary pass reads the PCG32 state from its LDS slot");
     extern __shared__ unsigned long long lds_stack[];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
@@ -209,22 +317,19 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     const DCamera& C = P.cam;
     const bool valid = (i < C.width) && (j < C.height);
     Counts cnt{};
-    const lds_crec* top = stage_top_records(P, lds_stack);
 #if MYRT_PIXLDS
-    // this wave's [kPixSlots][64] slab after the stacks and the near-root records
-    lds_f64* pacc = (lds_f64*)(lds_u64*)(lds_stack + (size_t)blockDim.x * kLds +
-                                         (size_t)(blockDim.x >> 6) * P.lds_top_n * 8) + wave * (kPixSlots * 64) + lane;
+    // this wave's [kPixSlots][64] slab after the stacks
+    lds_f64* pacc = (lds_f64*)(lds_u64*)(lds_stack + (size_t)blockDim.x * kLds) + wave * (kPixSlots * 64) + lane;
 #endif
     if (valid) {
         MYRT_STACK(st, lds_stack);
         st.uni_spill = !BOUNCE || MYRT_BOUNCE_UNI_SPILL;
-        st.top = top;
-        st.top_n = P.lds_top_n;
         PCG32 rng(pixel_seed(i, j));
         V3 pixel = v3(0, 0, 0);
         const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
         const int n = C.n;
         int sampleIndex = 0;
+        bool deferred = false;
         for (int sy = 0; sy < n && sampleIndex < C.samples; ++sy) {
             for (int sx = 0; sx < n; ++sx) {
                 const double xi1 = rng.nextFloat();
@@ -270,7 +375,8 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                 // in LDS while the rays are traced, so they are not live - spilled - across the
                 // walks; the memory clobber makes the reloads real loads.
                 if (!BOUNCE) pacc[3 * 64] = __builtin_bit_cast(double, rng.state);
-                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt, pacc + 3 * 64);
+                const V3 col = trace_path<COUNT, BOUNCE, UNI, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt,
+                                                                     pacc + 3 * 64, i, j, &deferred);
                 asm volatile("" ::: "memory");
                 if (!BOUNCE) {
                     rng.state = __builtin_bit_cast(unsigned long long, (double)pacc[3 * 64]);
@@ -293,21 +399,9 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
         pixel = v3(pacc[0], pacc[64], pacc[128]);
 #endif
         const V3 px = pixel / (double)C.samples;
-        const size_t row = out_row_of(P, chunk, rowInChunk);
-        const size_t o = row * (size_t)C.width + i;
-        if (P.out_rgb) {
-            P.out_rgb[o * 3 + 0] = px.x;
-            P.out_rgb[o * 3 + 1] = px.y;
-            P.out_rgb[o * 3 + 2] = px.z;
-        }
-        if (P.out_rgba8) {                                           // RayTracer.swift:186-195
-            const double cx = fmin(fmax(px.x, 0.0), 255.0), cy = fmin(fmax(px.y, 0.0), 255.0),
-                         cz = fmin(fmax(px.z, 0.0), 255.0);
-            const unsigned packed = (unsigned)(unsigned char)cx | ((unsigned)(unsigned char)cy << 8) |
-                                    ((unsigned)(unsigned char)cz << 16) | (255u << 24);
-            reinterpret_cast<unsigned*>(P.out_rgba8)[o] = packed;
-        }
+        if (!(QUEUE && deferred)) store_pixel(P, i, j, px);          // RayTracer.swift:186-195
 #if MYRT_WAVE_TIMES >= 2
+        const size_t o = out_row_of(P, chunk, rowInChunk) * (size_t)C.width + i;
         if (P.wave_times && P.out_rgb) {        // debug: per-lane walk iterations instead of the colour
             P.out_rgb[o * 3 + 0] = (double)cnt.it_closest;
             P.out_rgb[o * 3 + 1] = (double)cnt.it_shadow;
@@ -363,6 +457,105 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                 atomicAdd(&P.counters[18 + 5 * k], v2); atomicAdd(&P.counters[19 + 5 * k], v3);
                 atomicAdd(&P.counters[20 + 5 * k], v4);
             }
+        }
+    }
+}
+
+}  // namespace dev
+}  // namespace myrt
+
+namespace myrt {
+namespace dev {
+// One level of the compacted bounce render: the rays trace(depth = level) of every queued
+// sample, one lane per ray, waves taking 64 records at a time from the level's queue.
+// A mirror/conductor hit below maxRecursionDepth queues level + 1 (its own Lo follows after
+// the shadow walks); any other end resolves the sample backward through the records of its
+// ancestors and stores the pixel.  The last level's last wave zeroes the queue words.
+#ifndef MYRT_QUEUE_WPE
+#define MYRT_QUEUE_WPE 4
+#endif
+template <bool UNI>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_WPE))) void k_bounce(RenderParams P,
+                                                                                                    int level) {
+    extern __shared__ unsigned long long lds_stack[];
+    const int lane = threadIdx.x & 63;
+    Counts cnt{};
+    const unsigned long long n =
+        __hip_atomic_load(&P.counters[kQueueCount + level], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long lbase = (long long)(level - 1) * P.bounce_cap;
+    MYRT_STACK(st, lds_stack);
+    st.uni_spill = true;
+    for (;;) {
+        unsigned base = 0;
+        if (lane == 0) base = (unsigned)atomicAdd(&P.counters[kQueueGrab + level], 64ull);
+        base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+        if (base >= n) break;
+        if (base + lane >= n) continue;
+        const long long g = lbase + base + lane;
+        const BounceRec& R = P.bounce[g];
+        const V3 o = ld3(R.o), d = ld3(R.d);
+        const double time = UNI ? 0.0 : R.time;
+        V3 L;
+        bool ends = true;
+        if (!P.has_tlas) {
+            L = v3(0, 0, 0);
+        } else {
+            const V3 inv = rcp(d);
+            Hit h;
+            if (UNI) uni_closest<false>(P, o, d, inv, 0.0, h, st, cnt);
+            else intersect_closest<false>(P, o, d, inv, 0.0, time, h, st, cnt);
+            if (h.inst < 0) {
+                L = ld3(P.background);
+            } else {
+                V3 p, Ngeo;
+                hit_geometry<false>(P, o, d, time, h, p, Ngeo, cnt);
+                const DInstance& I = P.insts[h.inst];
+                const DMaterial& M = P.mats[max(0, min(P.num_mats - 1, I.material - 1))];
+                const bool frontFacing = dot(d, Ngeo) < 0;
+                const V3 N = frontFacing ? Ngeo : -Ngeo;
+                const bool computeDirect = !(M.ior > 0) || frontFacing;
+                V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+                const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && level < P.max_depth;
+                const long long q = queue_reserve(P, level + 1, want);
+                if (q >= 0) {
+                    const BounceRec& Rs = P.bounce[g];
+                    PCG32 r = PCG32::resume(Rs.rng, pixel_seed(Rs.i, Rs.j));
+                    queue_write(P, q, M, d, N, p, r, Rs.time, Rs.i, Rs.j, (int)g);
+                    cnt.secondary++;
+                }
+                auto none = []() {};
+                if (computeDirect) point_lights<false, UNI>(P, M, N, p, d, time, st, cnt, Lo, none, none);
+                if (q >= 0) {
+                    queue_write_lo(P, q, Lo);
+                    ends = false;
+                } else {
+                    L = isfin(Lo) ? Lo : v3(0, 0, 0);
+                }
+            }
+        }
+        if (ends) {      // back through the ancestors: Lo_k + M_k * L_(k+1), NaN guard per level
+            long long r = g;
+            int pi = 0, pj = 0;
+            for (;;) {
+                const BounceRec& A = P.bounce[r];
+                const V3 Lo = ld3(A.Lo) + ld3(A.M) * L;
+                L = isfin(Lo) ? Lo : v3(0, 0, 0);
+                if (A.parent < 0) { pi = A.i; pj = A.j; break; }
+                r = A.parent;
+            }
+            const V3 pixel = v3(0.0 + L.x, 0.0 + L.y, 0.0 + L.z);   // the sample sum (one sample)
+            store_pixel(P, pi, pj, pixel / (double)P.cam.samples);
+        }
+    }
+    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
+                             s2 = wave_sum(cnt.shadow_traced);
+    if (lane == 0) {
+        if (s0) atomicAdd(&P.counters[0], s0);
+        if (s1) atomicAdd(&P.counters[1], s1);
+        if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
+        if (level == P.max_depth) {     // every wave of the last level is past its last grab
+            if (atomicAdd(&P.counters[kQueueDone], 1ull) == (unsigned long long)gridDim.x - 1)
+                for (int k = kQueueDone; k < kCounterWords; ++k) atomicExch(&P.counters[k], 0ull);
         }
     }
 }
@@ -437,6 +630,13 @@ constexpr int kRenderBatches = 8;   // rt_render: chunk batches per replica (pro
 // compute units the previous frame's slowest tiles leave idle (tools/probe_overlap.py).
 constexpr int kInFlight = RT_MAX_IN_FLIGHT;
 constexpr int kSubmitDmaDefault = 0;   // rt_render_submit delivery (MYRT_SUBMIT_DMA, submit_impl)
+// Queued bounce rays of one stream's renders (BounceRec, levels x records per level)
+struct BounceArena {
+    BounceRec* recs = nullptr;
+    int64_t cap = 0;                               // records allocated
+};
+// Compacted bounce render: device bytes one launch may take for its queues (else the megakernel)
+constexpr int64_t kQueueBytesCap = 16ll << 30;
 struct Flight {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
@@ -448,7 +648,9 @@ struct Flight {
     uint8_t* stage_rgba = nullptr;
     int64_t stage_px = 0;
     bool counters_zero = false;
+    bool counters_valid = false;                   // host_counters hold this render's counts (k_counters_out ran)
     bool used = false;                             // this replica took part in the render
+    BounceArena arena;                             // compacted bounce render queues of this slot
 };
 
 struct DeviceReplica {
@@ -483,6 +685,8 @@ struct DeviceReplica {
     double* host_rgb = nullptr; uint8_t* host_rgba = nullptr; int64_t host_cap_px = 0;   // pinned
     std::vector<hipEvent_t> batch_done, batch_copied;
     int64_t bytes = 0;
+    int cus = 256;                            // compute units (k_bounce grid)
+    BounceArena arena;                        // compacted bounce queues of the replica stream
     WaveBuffers wave;                         // wavefront-pipeline queues (grown on demand)
     Flight fl[kInFlight];                     // rt_render_submit slots
 };
@@ -501,6 +705,7 @@ struct rt_scene {
         std::chrono::steady_clock::time_point t0;
         int64_t primary = 0;
         bool concurrent = true;                   // on the slot's own stream (else the replica stream)
+        bool waiting = false;                     // a thread is blocked in rt_render_wait on it
     } flights[RT_MAX_IN_FLIGHT];
     int64_t next_ticket = 0;
 };
@@ -521,6 +726,7 @@ static void free_replica(DeviceReplica& r) {
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart); (void)hipFree(r.wave_times);
     (void)hipFree(r.deep);
+    (void)hipFree(r.arena.recs);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.counters_ready) (void)hipEventDestroy(r.counters_ready);
@@ -534,6 +740,7 @@ static void free_replica(DeviceReplica& r) {
         (void)hipFree(f.counters);
         (void)hipFree(f.stage_rgb);
         (void)hipFree(f.stage_rgba);
+        (void)hipFree(f.arena.recs);
         if (f.host_counters) (void)hipHostFree(f.host_counters);
     }
     if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -582,6 +789,11 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
     if ((rc = upload(S.alights, &r.alights, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.jitter, &r.jitter, r.bytes)) != RT_OK) return rc;
     HIP_TRY(hipMalloc((void**)&r.counters, kCounterWords * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(r.counters, 0, kCounterWords * sizeof(unsigned long long)));
+    if (hipDeviceGetAttribute(&r.cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || r.cus <= 0) {
+        (void)hipGetLastError();
+        r.cus = 256;
+    }
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&r.copy_stream, hipStreamNonBlocking));
     r.batch_done.resize(kRenderBatches);
@@ -600,6 +812,8 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
         HIP_TRY(hipEventCreate(&f.ev1));
         HIP_TRY(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
         HIP_TRY(hipMalloc((void**)&f.counters, kCounterWords * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(f.counters, 0, kCounterWords * sizeof(unsigned long long)));
+        f.counters_zero = true;
         HIP_TRY(hipHostMalloc((void**)&f.host_counters, kCounterWords * sizeof(unsigned long long),
                               hipHostMallocMapped));
         HIP_TRY(hipHostGetDevicePointer((void**)&f.host_counters_dev, f.host_counters, 0));
@@ -693,10 +907,6 @@ static int32_t env_int(const char* name, int32_t def, int32_t lo, int32_t hi) {
     return std::min(hi, std::max(lo, (int32_t)std::atoi(v)));
 }
 
-// Near-root BLAS records kept in LDS per wave (device.h stage_top_records): 31 = the top 5
-// levels; with the 16-entry LDS stack a wave then holds 10 KB, 16 waves fill 160 KB.
-constexpr int32_t kLdsTopDefault = 0;    // measured no gain; its LDS now holds the pixel sums
-
 // Absolute pruning margin for rays whose origins lie within `origin_dist` of the scene
 // center (or inside the scene bounds): prune_k * (|o - v0| + t|d|) with both terms bounded
 // by the origin's distance plus the scene diagonal (scene.cpp, "pruning margin").
@@ -746,17 +956,6 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         P.prune_abs = prune_abs_for(S, dist_to_center(S, ce) + std::fabs(cam0.aperture_size));
     }
     P.fast_rcp = fast_rcp_for(S, 2.0);   // rendered directions are normalized (|d| <= 1 + 2^-50)
-    {   // FP32-enclosed slabs (slab32.h): eps rounded out, and a bound on every coordinate of an
-        // identity scene (every box of the unified walk lies inside the TLAS root box)
-        P.eps_up32 = f32slab::up(P.eps);
-        P.eps_dn32 = f32slab::dn(P.eps);
-        double bm = 0.0;
-        for (int k = 0; k < 3; ++k)
-            bm = std::max(bm, std::max(std::fabs(S.tlas_root_lo[k]), std::fabs(S.tlas_root_hi[k])));
-        P.bmax32 = f32slab::up(bm);
-        const char* fe = std::getenv("MYRT_F32");
-        P.use_f32 = (fe && fe[0] == '0') ? 0 : 1;
-    }
     for (int k = 0; k < 3; ++k) { P.background[k] = S.background[k]; P.ambient[k] = S.ambient[k]; }
     P.max_depth = S.max_depth;
     P.chunk_first = first; P.chunk_step = step;
@@ -772,22 +971,10 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         P.xcd_remap = xe ? std::atoi(xe) : std::max(2, P.cam.width / 960);
         const char* oe = std::getenv("MYRT_ROTATE");             // dispatch order: chunk rows rotated
         P.rot_slots = oe ? std::max(0, std::min(std::atoi(oe), nsel - 1)) : 0;
-        const char* se = std::getenv("MYRT_SCALAR");            // A/B switch: MYRT_SCALAR=0
-        P.scalar_nodes = (se && se[0] == '0') ? 0 : 1;
         const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0
         P.compact_limit = (ce && ce[0] == '0') ? 0 : (int32_t)S.compact_records;
-        const char* pe = std::getenv("MYRT_PACKET");            // A/B switch: MYRT_PACKET=0
-        P.packet = pe ? std::atoi(pe) : 3;                     // bit 0: closest hit, bit 1: any hit
-        // postponed leaves (device.h unified_walk_pl): the leaf block runs once this many lanes
-        // of the wave hold a leaf, or no lane can step; 0 = each leaf at once (A/B switch)
-        P.leaf_batch = env_int("MYRT_LEAF_BATCH", kLeafBatchDefault, 0, 64);
         const char* te = std::getenv("MYRT_CTRI");              // A/B switch: MYRT_CTRI=0
         P.ctris = (S.compact_tris && !(te && te[0] == '0')) ? r.ctris : nullptr;
-        // near-root records in LDS (megakernel; launch() clears it for the other kernels)
-        P.lds_top_n = dev::MYRT_LDS_TOP_CODE_ON
-                          ? (int32_t)std::min<int64_t>(env_int("MYRT_LDS_TOP", kLdsTopDefault, 0, kLdsTopMax),
-                                                       std::min<int64_t>(S.lds_top_records, P.compact_limit))
-                          : 0;
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
@@ -881,7 +1068,34 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
     return RT_OK;
 }
 
-static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P, hipStream_t stream, bool count) {
+// Compacted bounce render for this launch (render.hip k_bounce): mirror/conductor scenes whose
+// pixels trace one sample (Int(sqrt(spp)) == 1) with maxRecursionDepth <= kMaxQueueLevels;
+// `arena` grows to levels x pixels records (false: allocation refused or failed -> megakernel).
+static bool queue_arena(DeviceReplica& r, BounceArena* arena, RenderParams& P) {
+    if (!arena || env_int("MYRT_QUEUE", 0, 0, 1) == 0) return false;
+    if (P.cam.n != 1 || P.max_depth < 1 || P.max_depth > kMaxQueueLevels) return false;
+    const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;      // one ray per pixel and level at most
+    const int64_t need = px * P.max_depth;
+    if (need * (int64_t)sizeof(BounceRec) > kQueueBytesCap) return false;
+    if (need > arena->cap) {
+        (void)hipFree(arena->recs);
+        arena->recs = nullptr;
+        arena->cap = 0;
+        if (hipMalloc((void**)&arena->recs, (size_t)need * sizeof(BounceRec)) != hipSuccess) {
+            (void)hipGetLastError();
+            arena->recs = nullptr;
+            return false;
+        }
+        arena->cap = need;
+    }
+    P.bounce = arena->recs;
+    P.bounce_cap = px;
+    return true;
+}
+
+static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P0, hipStream_t stream, bool count,
+                      BounceArena* arena = nullptr) {
+    RenderParams P = P0;
     if (P.num_chunks == 0) return RT_OK;
     // dielectrics, area lights and maxRecursionDepth > kMaxDepthGPU: the full trace()
     // (render_full.h); it and spheres/planes exist only as megakernels
@@ -897,14 +1111,24 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     const int bt = block_threads();
     dim3 grid = render_grid(P, bt, dev::kTileW);
     dim3 block((unsigned)bt, 1, 1);
-    const size_t lds = (size_t)dev::kLds * bt * sizeof(int2) + (size_t)(bt / 64) * P.lds_top_n * sizeof(CRec) +
-                       (size_t)dev::kPixSlots * bt * sizeof(double);
+    const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long) + (size_t)dev::kPixSlots * bt * sizeof(double);
     const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
     // the unified walk needs an identity scene; reference-order counting uses the general walk
     const char* ue = std::getenv("MYRT_UNIFIED");
     const bool uni = P.identity && P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
 #define MYRT_LAUNCH(C_, B_, U_) hipLaunchKernelGGL((dev::render_kernel<C_, B_, U_>), grid, block, lds, stream, P)
-    if (count) {
+    if (bounce && !count && queue_arena(r, arena, P)) {
+        // primary + shadow rays of every pixel in the spill-free primary instantiation, then one
+        // k_bounce launch per level over the compacted queues
+        if (uni) hipLaunchKernelGGL((dev::render_kernel<false, false, true, true>), grid, block, lds, stream, P);
+        else hipLaunchKernelGGL((dev::render_kernel<false, false, false, true>), grid, block, lds, stream, P);
+        const dim3 qgrid((unsigned)(r.cus * 4 * MYRT_QUEUE_WPE)), qblock(64);
+        const size_t qlds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
+        for (int32_t level = 1; level <= P.max_depth; ++level) {
+            if (uni) hipLaunchKernelGGL((dev::k_bounce<true>), qgrid, qblock, qlds, stream, P, level);
+            else hipLaunchKernelGGL((dev::k_bounce<false>), qgrid, qblock, qlds, stream, P, level);
+        }
+    } else if (count) {
         if (bounce) { if (uni) MYRT_LAUNCH(true, true, true); else MYRT_LAUNCH(true, true, false); }
         else { if (uni) MYRT_LAUNCH(true, false, true); else MYRT_LAUNCH(true, false, false); }
     } else {
@@ -919,7 +1143,9 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
 extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
-const char* rt_version(void) { return "myraytracer_amd 0.1 (gfx950, fp64)"; }
+#define MYRT_STR2(x) #x
+#define MYRT_STR(x) MYRT_STR2(x)
+const char* rt_version(void) { return "myraytracer_amd 0.2 (abi " MYRT_STR(RT_ABI_VERSION) ", gfx950, fp64)"; }
 
 int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32_t n_devices, rt_scene** out) {
     if (!out) return fail(RT_ERR_INVALID_ARG, "out is NULL");
@@ -1004,7 +1230,7 @@ int32_t rt_render_device(rt_scene* s, int32_t slot, int32_t cam, int32_t first, 
     HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
     r.counters_zero = false;
     RenderParams P = make_params(s, r, cam, first, step, d_rgb, d_rgba8);
-    return launch(s, r, P, st, false);
+    return launch(s, r, P, st, false, &r.arena);
 }
 
 int32_t rt_stats_collect(rt_scene* s, int32_t slot, rt_stats* stats) {
@@ -1146,26 +1372,34 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
     const bool concurrent = !(s->host.has_dielectric || !s->host.alights.empty() || s->host.max_depth > kMaxDepthGPU) &&
                             use_megakernel();
     const auto t0 = std::chrono::steady_clock::now();
+    // the caller's buffers mapped for every replica BEFORE anything is launched: a replica
+    // that cannot map them must not leave the others' kernels writing into them
+    std::vector<double*> zrgb(D, nullptr);
+    std::vector<uint8_t*> zrgba(D, nullptr);
     for (int32_t k = 0; k < D; ++k) {
-        DeviceReplica& r = s->devs[k];
-        Flight& f = r.fl[q];
-        f.used = false;
-        const int32_t myFirst = first + k * step, myStep = step * D;
-        if (myFirst >= num_chunks_total(H)) continue;
-        HIP_TRY(hipSetDevice(r.device));
-        double* zrgb = nullptr;
-        uint8_t* zrgba = nullptr;
-        if ((out_rgb && hipHostGetDevicePointer((void**)&zrgb, out_rgb, 0) != hipSuccess) ||
-            (out_rgba8 && hipHostGetDevicePointer((void**)&zrgba, out_rgba8, 0) != hipSuccess)) {
+        if (first + k * step >= num_chunks_total(H)) continue;
+        HIP_TRY(hipSetDevice(s->devs[k].device));
+        if ((out_rgb && hipHostGetDevicePointer((void**)&zrgb[k], out_rgb, 0) != hipSuccess) ||
+            (out_rgba8 && hipHostGetDevicePointer((void**)&zrgba[k], out_rgba8, 0) != hipSuccess)) {
             (void)hipGetLastError();
             *not_pinned = true;
             return fail(RT_ERR_INVALID_ARG, "page-locked outputs are not mapped for this device");
         }
+    }
+    for (int32_t k = 0; k < D; ++k) s->devs[k].fl[q].used = false;
+    // delivery: 0 = the kernel stores the rows into the host buffer; 1 = rows rendered into
+    // device staging and copied by the DMA engine; 2 = staging only, not delivered
+    // (measurement switch MYRT_SUBMIT_DMA)
+    const int dma = env_int("MYRT_SUBMIT_DMA", kSubmitDmaDefault, 0, 2);
+    const bool counters_out = env_int("MYRT_SUBMIT_COUNTERS", 1, 0, 1) == 1;
+    const int32_t fail_at = env_int("MYRT_DEBUG_FAIL_REPLICA", -1, -1, 1 << 20);   // test hook
+    auto launch_one = [&](int32_t k) -> int32_t {
+        DeviceReplica& r = s->devs[k];
+        Flight& f = r.fl[q];
+        const int32_t myFirst = first + k * step, myStep = step * D;
+        HIP_TRY(hipSetDevice(r.device));
+        if (k == fail_at) return fail(RT_ERR_DEVICE, "injected launch failure (MYRT_DEBUG_FAIL_REPLICA)");
         hipStream_t st = concurrent ? f.stream : r.stream;
-        // delivery: 0 = the kernel stores the rows into the host buffer; 1 = rows rendered into
-        // device staging and copied by the DMA engine; 2 = staging only, not delivered
-        // (measurement switch MYRT_SUBMIT_DMA)
-        const int dma = env_int("MYRT_SUBMIT_DMA", kSubmitDmaDefault, 0, 2);
         int32_t nq = 0;
         for (int32_t c = myFirst; c < num_chunks_total(H); c += myStep) nq++;
         if (dma) {
@@ -1180,16 +1414,17 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         }
         if (!f.counters_zero) HIP_TRY(hipMemsetAsync(f.counters, 0, kCounterWords * sizeof(unsigned long long), st));
         f.counters_zero = false;
+        f.used = true;                                   // work may be queued on its stream from here on
         if (timing) HIP_TRY(hipEventRecord(f.ev0, st));
         f.timed = timing;
-        RenderParams P = make_params(s, r, cam, myFirst, myStep, dma ? (out_rgb ? f.stage_rgb : nullptr) : zrgb,
-                                     dma ? (out_rgba8 ? f.stage_rgba : nullptr) : zrgba);
+        RenderParams P = make_params(s, r, cam, myFirst, myStep, dma ? (out_rgb ? f.stage_rgb : nullptr) : zrgb[k],
+                                     dma ? (out_rgba8 ? f.stage_rgba : nullptr) : zrgba[k]);
         P.counters = f.counters;
         if (!dma) {                                      // rows at their places in the caller's buffer
             P.out_first = frame ? 0 : first;
             P.out_step = frame ? 1 : step;
         }                                                // else packed rows of this replica's chunks
-        const int32_t rc = launch(s, r, P, st, false);
+        const int32_t rc = launch(s, r, P, st, false, concurrent ? &f.arena : &r.arena);
         if (rc != RT_OK) return rc;
         if (dma == 1) {
             // chunk q of this replica = selection entry k + q*D = image chunk myFirst + q*myStep;
@@ -1213,13 +1448,34 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
             if (out_rgba8) HIP_TRY(copy(out_rgba8, f.stage_rgba, 4));
         }
         if (timing) HIP_TRY(hipEventRecord(f.ev1, st));
-        if (env_int("MYRT_SUBMIT_COUNTERS", 1, 0, 1) == 1) {
+        if (counters_out) {
             hipLaunchKernelGGL(dev::k_counters_out, dim3(1), dim3(64), 0, st, f.counters, f.host_counters_dev);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(f.done, st));
-        f.counters_zero = true;
-        f.used = true;
+        // the counters are zero again only when k_counters_out ran (it zeroes them behind its copy)
+        f.counters_zero = counters_out;
+        f.counters_valid = counters_out;
+        return RT_OK;
+    };
+    for (int32_t k = 0; k < D; ++k) {
+        if (first + k * step >= num_chunks_total(H)) continue;
+        const int32_t rc = launch_one(k);
+        if (rc != RT_OK) {
+            // replicas already launched write into the caller's buffers: drain them before the
+            // error returns (the caller may free the buffers), and leave the slot free
+            const std::string err = g_err;
+            for (int32_t j = 0; j <= k; ++j) {
+                Flight& f = s->devs[j].fl[q];
+                if (!f.used) continue;
+                (void)hipSetDevice(s->devs[j].device);
+                (void)hipStreamSynchronize(concurrent ? f.stream : s->devs[j].stream);
+                f.used = false;
+                f.counters_zero = false;
+            }
+            (void)hipGetLastError();
+            return fail(rc, err);
+        }
     }
     const int64_t n = (int64_t)std::sqrt((double)std::max(1, C.num_samples));
     fp.ticket = s->next_ticket++;
@@ -1237,6 +1493,10 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
     rt_scene::Pending& fp = s->flights[q];
     if (ticket < 0 || !fp.pending || fp.ticket != ticket)
         return fail(RT_ERR_INVALID_ARG, "unknown ticket, or already waited for");
+    // one waiter per ticket: the slot stays pending (no submit can reuse it) until that waiter
+    // has re-locked and read its counters; a second concurrent wait is refused
+    if (fp.waiting) return fail(RT_ERR_INVALID_ARG, "ticket is already being waited for by another thread");
+    fp.waiting = true;
     std::vector<std::pair<int, hipEvent_t>> evs;
     for (auto& r : s->devs)
         if (r.fl[q].used) evs.emplace_back(r.device, r.fl[q].done);
@@ -1247,6 +1507,7 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
         if (e == hipSuccess) e = hipEventSynchronize(de.second);
     }
     lock.lock();
+    fp.waiting = false;
     fp.pending = false;
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("render failed: ") + hipGetErrorString(e));
     double km = 0;
@@ -1254,8 +1515,9 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
     for (auto& r : s->devs) {
         Flight& f = r.fl[q];
         if (!f.used) continue;
+        // with MYRT_SUBMIT_COUNTERS=0 no counts came back: shadow/secondary stats are reported as 0
         const unsigned long long* c = f.host_counters;
-        sh += (int64_t)c[0]; se += (int64_t)c[1]; stc += (int64_t)c[kCounterShadowTraced];
+        if (f.counters_valid) { sh += (int64_t)c[0]; se += (int64_t)c[1]; stc += (int64_t)c[kCounterShadowTraced]; }
         float ms = 0;
         if (f.timed && hipEventElapsedTime(&ms, f.ev0, f.ev1) != hipSuccess) (void)hipGetLastError();
         km = std::max(km, (double)ms);
@@ -1422,7 +1684,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
                 P.out_first = frame ? 0 : first;
                 P.out_step = frame ? 1 : step;
             }
-            const int32_t lrc = launch(s, r, P, r.stream, false);
+            const int32_t lrc = launch(s, r, P, r.stream, false, &r.arena);
             if (lrc != RT_OK) return lrc;
             HIP_TRY(hipEventRecord(r.batch_done[b], r.stream));
             if (b == pl.nb - 1) {
@@ -1762,7 +2024,7 @@ int32_t rt_debug_wave_times(rt_scene* s, int32_t slot, int32_t cam, int32_t firs
     P.wave_times = r.wave_times;
     HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), r.stream));
     r.counters_zero = false;
-    if ((rc = launch(s, r, P, r.stream, false)) != RT_OK) return rc;
+    if ((rc = launch(s, r, P, r.stream, false, &r.arena)) != RT_OK) return rc;
     HIP_TRY(hipStreamSynchronize(r.stream));
     const int64_t n = std::min<int64_t>(waves, max_waves);
     if (out && n > 0) HIP_TRY(hipMemcpy(out, r.wave_times, (size_t)n * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost));

@@ -393,9 +393,9 @@ struct InstBuild { int blas; double M[16]; int material; D3 motion; double wlo[3
 // entries produced by `emit_leaf(first_prim_slot, count)` which returns the index of
 // the run's first entry.  Returns the root ref.
 // With topRecords > 0 the first min(topRecords, inner nodes) records are the inner nodes
-// nearest the root in breadth-first order (the kernels keep that prefix in LDS, device.h
-// Stack::top); the rest follow in preorder.  Record numbering is free: traversal order
-// depends only on the tree.
+// nearest the root in breadth-first order (the near-root records every ray reads sit in a
+// few adjacent lines); the rest follow in preorder.  Record numbering is free: traversal
+// order depends only on the tree.
 template <class EmitLeaf>
 static int32_t layout_bvh(const RefBVH& b, std::vector<WRec>& recs, EmitLeaf emit_leaf, int64_t topRecords = 0) {
     if (b.isLeaf(0) || (b.count[0] == 0 && b.nodesUsed == 0)) {
@@ -759,10 +759,10 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             return first;
         };
         bb.tri_first = (int64_t)S.tris.size();
-        // the first BLAS starts at record 0: its top records form the LDS-resident prefix
-        const int64_t top = S.recs.empty() ? kLdsTopMax : 0;
+        // the first BLAS starts at record 0 with a breadth-first prefix of its top levels
+        constexpr int64_t kTopRecords = 127;
+        const int64_t top = S.recs.empty() ? kTopRecords : 0;
         bb.root_ref = layout_bvh(bb.bvh, S.recs, emit, top);
-        if (top > 0) S.lds_top_records = std::min<int64_t>(kLdsTopMax, (int64_t)S.recs.size());
         bb.tri_end = (int64_t)S.tris.size();
         for (int k = 0; k < 3; ++k) { bb.root_lo[k] = bb.bvh.lo[k]; bb.root_hi[k] = bb.bvh.hi[k]; }
         bb.bvh = RefBVH();   // free host copy

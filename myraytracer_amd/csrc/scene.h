@@ -55,7 +55,6 @@ struct HostScene {
     std::vector<WRec> recs;
     std::vector<CRec> crecs;               // float32-bound copy of the BLAS records (if exact)
     int64_t compact_records = 0;           // crecs.size() (kept after the host copy is dropped)
-    int64_t lds_top_records = 0;           // records [0, n): the first BLAS's top, breadth-first
     std::vector<TriRec> tris;
     std::vector<CTri> ctris;               // float32-vertex copy of tris (if every vertex is exact)
     bool compact_tris = false;

@@ -81,6 +81,10 @@ static void put_utf8(std::string& out, unsigned long cp) {
     }
 }
 
+// Deepest array/object (JSON) or element (XML) nesting the decoders accept: they recurse once
+// per level, so an unbounded '[[[[...' would overflow the host stack instead of failing.
+constexpr int kMaxNesting = 512;
+
 // ----------------------------------------------------------------------------- JSON
 class Json {
   public:
@@ -94,14 +98,21 @@ class Json {
 
   private:
     const char *p_, *e_;
+    int depth_ = 0;
     void ws() { while (p_ < e_ && space(*p_)) ++p_; }
     [[noreturn]] void bad(const char* what) { fail(std::string("scene decode failed: ") + what); }
+    Value nested(bool obj) {
+        if (++depth_ > kMaxNesting) bad("nesting too deep");
+        Value v = obj ? object() : array();
+        --depth_;
+        return v;
+    }
     Value value() {
         ws();
         if (p_ >= e_) bad("unexpected end of JSON");
         const char c = *p_;
-        if (c == '{') return object();
-        if (c == '[') return array();
+        if (c == '{') return nested(true);
+        if (c == '[') return nested(false);
         if (c == '"') { Value v; v.kind = Value::Str; v.str = string(); return v; }
         if (c == 't' || c == 'f' || c == 'n') return literal();
         return number();
@@ -242,6 +253,7 @@ class Xml {
 
   private:
     const char *p_, *e_;
+    int depth_ = 0;
     [[noreturn]] void bad(const char* what) { fail(std::string("scene decode failed: XML: ") + what); }
     bool starts(const char* w) const {
         const size_t n = std::strlen(w);
@@ -288,6 +300,8 @@ class Xml {
     // One element -> Str (no attributes and no children: its text) or Obj ("_attr" keys, the
     // children by tag - repeats become an Arr - and "_data" = the text before the first child)
     Value element(std::string& tag) {
+        if (++depth_ > kMaxNesting) bad("nesting too deep");
+        struct Leave { int& d; ~Leave() { --d; } } leave{depth_};
         ++p_;   // '<'
         tag = name();
         Value v;

@@ -73,6 +73,7 @@ def test_error_codes_without_compute():
     m = A.rt_ply_mesh()
     assert lib.rt_ply_load(b"/nonexistent.ply", C.byref(m)) == A.RT_ERR_PLY
     assert lib.rt_version().startswith(b"myraytracer_amd")
+    assert b"(abi 2," in lib.rt_version()          # RT_ABI_VERSION (rtcore.h)
 
 
 def test_product_fails_loudly_without_gpu():

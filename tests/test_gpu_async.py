@@ -125,3 +125,66 @@ def test_submit_errors():
     eng.wait(t)
     assert np.array_equal(outs[Q], rgba)
     eng.close()
+
+
+def test_failed_replica_launch_drains_and_frees_the_slot(monkeypatch):
+    """A launch that fails on replica k > 0 (forced: MYRT_DEBUG_FAIL_REPLICA) must not leave
+    replicas 0..k-1 writing into the caller's buffers behind an error: they are drained before
+    rt_render_submit returns, and the slot is free again (every slot still takes a render)."""
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 96, 72)
+    W, H = sc.cameras[0].image_resolution
+    eng = M.RayTracerEngine(sc, devices=[0, 0, 0])
+    want = _sync(eng, 0, 0, 1, H, W)
+    out = M.pinned_array((H, W, 4), np.uint8)
+    out.fill(0)
+    monkeypatch.setenv("MYRT_DEBUG_FAIL_REPLICA", "1")
+    with pytest.raises(M.RenderError) as e:
+        eng.submit_into(0, 0, 1, rgba=out, frame_layout=True)
+    assert e.value.code == A.RT_ERR_DEVICE and "injected" in str(e.value)
+    with pytest.raises(M.RenderError) as e:                  # rt_render_ex shares the path
+        eng.render_into(0, 0, 1, rgba=out, frame_layout=True)
+    assert e.value.code == A.RT_ERR_DEVICE
+    # replica 0's rows (chunks 0, 3, 6, ...) were rendered and drained; nothing else was written
+    rows = np.zeros(H, bool)
+    for c in range(0, (H + 7) // 8, 3):
+        rows[8 * c: 8 * c + 8] = True
+    snap = out.copy()
+    assert np.array_equal(snap[rows], want[1][rows]) and np.all(snap[~rows] == 0)
+    monkeypatch.delenv("MYRT_DEBUG_FAIL_REPLICA")
+    outs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(A.RT_MAX_IN_FLIGHT)]
+    ts = [eng.submit_into(0, 0, 1, rgba=o, frame_layout=True) for o in outs]
+    for t, o in zip(ts, outs):
+        eng.wait(t)
+        assert np.array_equal(o, want[1])
+    assert np.array_equal(out, snap)                         # no late writes from the failed submits
+    eng.close()
+
+
+def test_concurrent_waits_on_one_ticket():
+    """Two threads waiting on the same ticket: exactly one gets the render's stats, the other
+    an error (it must never return the counts of a later render reusing the slot)."""
+    import threading
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 400, 300)
+    W, H = sc.cameras[0].image_resolution
+    eng = M.RayTracerEngine(sc)
+    want = _sync(eng, 0, 0, 1, H, W)[2]
+    for _ in range(5):
+        out = M.pinned_array((H, W, 4), np.uint8)
+        t = eng.submit_into(0, 0, 1, rgba=out, frame_layout=True)
+        res = []
+
+        def waiter():
+            try:
+                res.append(("ok", eng.wait(t)))
+            except M.RenderError as e:
+                res.append(("err", e.code))
+        th = [threading.Thread(target=waiter) for _ in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        oks = [r for k, r in res if k == "ok"]
+        assert len(oks) == 1 and len(res) == 2
+        assert oks[0].shadow_rays == want.shadow_rays
+        assert [r for k, r in res if k == "err"] == [A.RT_ERR_INVALID_ARG]
+    eng.close()

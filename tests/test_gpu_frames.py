@@ -202,3 +202,23 @@ def test_bench_strong_split_two_ranks_gathers_the_same_frame():
     assert one["gather"]["rows_complete"] and two["gather"]["rows_complete"]
     assert two["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
     assert two["rays"]["per_step"] == one["rays"]["per_step"]
+
+
+@pytest.mark.timeout(480)
+def test_bench_strong_split_eight_ranks_on_one_gpu():
+    """The C4 process path at N = 8 (Object+Extension.swift:75-82): `bench.py --gpus 8` with
+    every rank pinned to this GPU (MYRT_BENCH_DEVICE=0, 32 / 8 = 4 hardware queues per rank),
+    C2, 3 steps: 8 processes, 16 shared registered framebuffers, chunk c on rank c mod 8.  The
+    gathered frame is complete and bit-identical to the 1-GPU frame, and the line carries
+    every rank's timing."""
+    common = ["--config", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-side-paths"]
+    one = _bench(["--gpus", "1"] + common, {})
+    eight = _bench(["--gpus", "8"] + common, {"MYRT_BENCH_DEVICE": "0"})
+    assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
+    assert eight["config"]["hw_queues"] == "4"
+    assert eight["gather"]["rows_complete"]
+    assert eight["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
+    assert eight["rays"]["per_step"] == one["rays"]["per_step"]
+    pr = eight["per_rank"]
+    assert len(pr["ms_per_step"]) == 8 and pr["max_ms"] >= pr["min_ms"] > 0
+    assert sum(pr["rows"]) == 600 and all(x > 0 for x in pr["submit_us_per_frame"])

@@ -170,6 +170,19 @@ def test_bad_documents(data, fmt):
     assert nf.rc == A.RT_ERR_SCENE_FILE and nf.err
 
 
+@pytest.mark.parametrize("data,fmt", [("[" * 300000 + "]" * 300000, A.RT_SCENE_FORMAT_JSON),
+                                      ('{"a":' * 200000 + "1" + "}" * 200000, A.RT_SCENE_FORMAT_JSON),
+                                      ("<a>" * 200000 + "</a>" * 200000, A.RT_SCENE_FORMAT_XML)])
+def test_deep_nesting_fails_instead_of_overflowing_the_stack(data, fmt):
+    """The recursive decoders stop at 512 levels with RT_ERR_SCENE_FILE (a few hundred
+    thousand levels used to overflow the host stack and crash the process)."""
+    nf = NativeFile(data=data, fmt=fmt)
+    assert nf.rc == A.RT_ERR_SCENE_FILE and "nesting too deep" in nf.err, nf.err
+    ok = NativeFile(data='{"Scene": {"x": ' + "[" * 500 + "]" * 500 + "}}", fmt=A.RT_SCENE_FORMAT_JSON)
+    assert ok.rc == 0, ok.err
+    ok.close()
+
+
 def test_missing_file():
     nf = NativeFile(path="/nonexistent/scene.json")
     assert nf.rc == A.RT_ERR_SCENE_FILE and "cannot open" in nf.err
