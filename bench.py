@@ -66,7 +66,10 @@ def parse():
     # 2000 C3 frames = ~1.3 s timed at N = 1: long enough for an outside GPU-busy sampler
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
+    p.add_argument("--config", default="c3", choices=["c2", "c3", "c5", "c3i", "c3g"],
+                   help="c3 (default, BASELINE configs[2]); c2 / c5 (configs[1] / [4]); c3i: C3 as 25 mesh "
+                        "instances with transforms (literal TLAS->BLAS walk); c3g: C3 with glass spheres and two "
+                        "area lights (full trace() kernels)")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong (default): one frame per step split over the ranks (C4); "
                         "weak: every rank renders a full frame per step")
@@ -174,6 +177,14 @@ def main():
     elif args.config == "c2":
         scene = scenes.scene_c2(path_dir=args.cache)
         workload = "C2: ~69k-tri PLY bunny stand-in, 800x600, 1 spp, 1 point light"
+    elif args.config == "c3i":
+        scene = scenes.scene_c3_instanced(path_dir=args.cache)
+        workload = ("C3i: C3's geometry as 25 mesh instances with non-identity transforms (terrain + 24 instances "
+                    "of one icosphere BLAS), 1920x1080, 1 spp, 1 point light, shadows: the literal TLAS->BLAS walk")
+    elif args.config == "c3g":
+        scene = scenes.scene_c3_glass(path_dir=args.cache)
+        workload = ("C3g: C3's geometry with 24 glass (dielectric, Beer) spheres, 1 point + 2 area lights, "
+                    "1920x1080, 1 spp, maxRecursionDepth 4: full trace() kernels")
     else:
         scene = scenes.scene_c5(path_dir=args.cache)
         workload = "C5: ~10M-tri (2 meshes, mirror spheres), 3840x2160, depth-4 reflections"

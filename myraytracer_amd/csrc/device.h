@@ -693,7 +693,25 @@ __device__ __forceinline__ bool unified_leaf(const RenderParams& P, int ref, Sta
             tri_closest(T, o, d, tlo, eps, h, t, T.prim, P.fast_rcp);   // prim = owning instance
             return false;
         };
+#ifndef MYRT_LEAF_PREFETCH
+#define MYRT_LEAF_PREFETCH 0
+#endif
         auto run = [&](const auto* tris) -> bool {
+            if (MYRT_LEAF_PREFETCH) {
+                // both triangles of a pair are loaded before the first test, so the second load's
+                // latency hides behind the first test; tris[t + 1] is always readable (the device
+                // arrays carry one zeroed record past the end, render.hip upload_padded).  The
+                // tests themselves stay in leaf order (strict <, RTContext.swift:573-597).
+                for (int t = e;; t += 2) {
+                    const auto T0 = tris[t];
+                    const auto T1 = tris[t + 1];
+                    if (test(T0, t)) return true;
+                    if (T0.last) break;
+                    if (test(T1, t + 1)) return true;
+                    if (T1.last) break;
+                }
+                return false;
+            }
             for (int t = e;; ++t) {
                 const auto T = tris[t];          // by value: `last` arrives with the vertices
                 if (test(T, t)) return true;

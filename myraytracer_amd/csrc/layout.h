@@ -96,15 +96,15 @@ struct DTlasLeafEntry { int32_t inst; int32_t last; };
 // A queued mirror/conductor bounce ray (compacted bounce render, render.hip k_bounce): the
 // child trace(depth + 1) of one sample plus what its parent level adds back,
 // Lo_parent + M_parent * trace(depth + 1) (Object+Extension.swift:189-206, 252-275).
-// Level-k records live at [(k - 1) * cap, k * cap) of RenderParams::bounce.
+// The level-k record of a pixel sits at [(k - 1) * cap + pixel slot] of RenderParams::bounce,
+// so its parent is the same slot one level up.
 struct alignas(128) BounceRec {
     double o[3], d[3];        // the reflected ray (origin p + N * shadowRayEpsilon, tMin 0)
     double Lo[3], M[3];       // the parent level's radiance and its mirror/Fresnel multiplier
     unsigned long long rng;   // the sample's PCG32 state after the parent's draws (roughness)
     double time;              // the sample's ray time (instance motion)
     int32_t i, j;             // pixel
-    int32_t parent;           // record of the parent level (global index), -1 = the primary sample
-    int32_t pad;
+    int32_t pad[2];
 };
 static_assert(sizeof(BounceRec) == 128, "BounceRec is one 128-B line");
 
@@ -162,10 +162,16 @@ struct RenderParams {
     // a launch covers selected chunks [slot_base, slot_base + gridDim.x / tiles-per-chunk)
     void* deep;
     int32_t slot_base;
-    // compacted bounce render (render.hip k_bounce): queued bounce rays, `bounce_cap` records per
-    // level; nullptr = the bounce megakernel
+    // compacted bounce render (render.hip k_bounce); bounce == nullptr: the bounce megakernel.
+    // Ray records by pixel slot: [level - 1][tile * 64 + lane] (tile = wave of the primary launch);
+    // bmask[level - 1][tile] = the tile's lanes with a ray at that level; bact = k_qscan's list of
+    // the level's tiles that have rays ([0, A) tile ids, [bounce_tiles, bounce_tiles + A) the
+    // exclusive prefix of their ray counts)
     BounceRec* bounce;
-    int64_t bounce_cap;
+    unsigned long long* bmask;
+    uint32_t* bact;
+    int64_t bounce_cap;              // records per level = bounce_tiles * 64
+    int32_t bounce_tiles;
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
     unsigned long long* counters;    // [0] shadow rays cast, [1] secondary rays, [2..12] work counters,
@@ -175,10 +181,10 @@ struct RenderParams {
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters
-// Compacted bounce render: words [32, 64) of the counters.  Level k (1..kMaxQueueLevels) has its
-// queue length at kQueueCount + k and its work-grab cursor at kQueueGrab + k; word kQueueDone
-// counts the last level's finished waves (the last one zeroes the queue words for the next launch).
-constexpr int kQueueDone = 32, kQueueCount = 32, kQueueGrab = 48;
+// Compacted bounce render: words [32, 64) of the counters.  Level k (1..kMaxQueueLevels): its ray
+// count at kQueueCount + k and its number of tiles with rays at kQueueTiles + k (k_qscan);
+// k_queue_reset zeroes them (and the tile masks) after the last level.
+constexpr int kQueueCount = 32, kQueueTiles = 48;
 constexpr int kMaxQueueLevels = 15;
 constexpr int kCounterShadowTraced = 13;
 constexpr int kMaxDepthGPU = 16;     // trace() levels kept in private memory per lane (deeper: RenderParams::deep)

@@ -84,31 +84,20 @@ __device__ __forceinline__ void point_lights(const RenderParams& P, const DMater
 // ---- compacted bounce render (mirror/conductor scenes, one traced sample per pixel) --------
 // The primary pass renders every pixel's primary ray and shadow rays in the spill-free
 // primary instantiation; a lane whose hit is a mirror or conductor below maxRecursionDepth
-// appends its reflected ray to the level-1 queue instead of tracing it (wave ballot + popc
-// prefix, one atomic per wave).  k_bounce traces one level's queue, appending the next level;
-// a ray that ends resolves its sample backward through its ancestors' records with the
-// per-level NaN guard, Lo_k + M_k * L_(k+1) (Object+Extension.swift:189-206, 252-283), and
-// stores the pixel.  Same operations on the same values as the recursion: identical frames.
-
-// Queue slots for the lanes of this wave that `want` a ray at `level`: returns the record's
-// global index, or -1.
-__device__ __forceinline__ long long queue_reserve(const RenderParams& P, int level, bool want) {
-    const unsigned long long m = __ballot(want);
-    if (m == 0) return -1;
-    const int leader = __builtin_ctzll(m);
-    unsigned base = 0;
-    if ((int)(threadIdx.x & 63) == leader)
-        base = (unsigned)atomicAdd(&P.counters[kQueueCount + level], (unsigned long long)__popcll(m));
-    base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
-    const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-    return want ? (long long)(level - 1) * P.bounce_cap + (long long)(base + below) : -1ll;
-}
+// writes its reflected ray to its pixel's level-1 record instead of tracing it, and the wave
+// stores the ballot of those lanes as its tile mask.  Per level, k_qscan lists the tiles with
+// rays and prefixes their counts, and k_bounce traces the level's rays in batches of 64
+// consecutive rays in tile order (a batch holds neighbouring pixels' rays: coherent walks),
+// writing the next level the same way.  A ray that ends resolves its sample backward through
+// its pixel's records with the per-level NaN guard, Lo_k + M_k * L_(k+1)
+// (Object+Extension.swift:189-206, 252-283), and stores the pixel: the operations of the
+// recursion on the same values, so frames are identical.  No same-address atomics: returning
+// atomics on one counter from thousands of waves serialize (~85 ns each, measured).
 
 // The reflected ray of a mirror/conductor hit and its multiplier (Object+Extension.swift:
 // 189-206, 252-275) into record q; the parent's Lo follows after its shadow walks.
 __device__ __forceinline__ void queue_write(const RenderParams& P, long long q, const DMaterial& M, const V3& d,
-                                            const V3& N, const V3& p, PCG32& rng, double time, int i, int j,
-                                            int parent) {
+                                            const V3& N, const V3& p, PCG32& rng, double time, int i, int j) {
     V3 mult;
     if (M.type == RT_MAT_MIRROR) {
         mult = ld3(M.mirror);
@@ -133,7 +122,6 @@ __device__ __forceinline__ void queue_write(const RenderParams& P, long long q, 
     R.rng = rng.state;
     R.time = time;
     R.i = i; R.j = j;
-    R.parent = parent;
 }
 __device__ __forceinline__ void queue_write_lo(const RenderParams& P, long long q, const V3& Lo) {
     BounceRec& R = P.bounce[q];
@@ -162,13 +150,14 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, int i, int j,
 // backward with the same per-level NaN guard, so the result is the recursive one.
 // `rng_slot`: this lane's LDS slot for the PCG32 state (BOUNCE: the state waits there while
 // the rays are traced instead of being live - spilled - across the walks; nullptr = keep it)
-// QUEUE (primary pass of the compacted bounce render, !BOUNCE): a mirror/conductor hit queues
-// its reflected ray (level 1) and sets `deferred`; k_bounce delivers that pixel.  The PCG32
-// state is then read from rng_slot (the caller parks it there) and (i, j) give its stream.
+// QUEUE (primary pass of the compacted bounce render, !BOUNCE): a mirror/conductor hit writes
+// its reflected ray to its pixel's level-1 record (slot `qtile * 64 + lane`, qtile = this wave's
+// tile) and sets `deferred`; k_bounce delivers that pixel.  The PCG32 state is read from
+// rng_slot (the caller parks it there) and (i, j) give its stream.
 template <bool COUNT, bool BOUNCE, bool UNI, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
                          Counts& c, __attribute__((address_space(3))) double* rng_slot, int i = 0, int j = 0,
-                         bool* deferred = nullptr) {
+                         bool* deferred = nullptr, int qtile = 0) {
     static_assert(!(QUEUE && BOUNCE), "the queued primary pass has no bounce loop");
     auto park = [&]() { if (BOUNCE && rng_slot) *rng_slot = __builtin_bit_cast(double, rng.state); };
     auto unpark = [&]() {
@@ -203,11 +192,16 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         long long q = -1;
         if (QUEUE) {     // the bounce ray is formed before the shadow walks: only q stays live
             const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && P.max_depth > 0;
-            q = queue_reserve(P, 1, want);
-            if (q >= 0) {
-                PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*rng_slot), pixel_seed(i, j));
-                queue_write(P, q, M, d, N, p, r, time, i, j, -1);
-                c.secondary++;
+            const unsigned long long m = __ballot(want);
+            if (m) {
+                if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) P.bmask[qtile] = m;
+                if (want) {
+                    q = (long long)qtile * 64 + (threadIdx.x & 63);
+                    PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*rng_slot),
+                                            pixel_seed(i, j));
+                    queue_write(P, q, M, d, N, p, r, time, i, j);
+                    c.secondary++;
+                }
             }
         }
         if (computeDirect) point_lights<COUNT, UNI>(P, M, N, p, d, time, st, c, Lo, park, unpark);
@@ -276,8 +270,12 @@ typedef __attribute__((address_space(3))) double lds_f64;
 #ifndef MYRT_BOUNCE_WPE
 #define MYRT_BOUNCE_WPE 6   // the bounce (mirror/conductor) instantiation: 6 waves/SIMD (80 VGPRs; C5 -7.5 %)
 #endif
+#ifndef MYRT_QPRIM_WPE
+#define MYRT_QPRIM_WPE 4    // the queued primary pass of the compacted bounce render
+#endif
 #if MYRT_MEGA_WPE > 0
-#define MYRT_MEGA_ATTR __attribute__((amdgpu_waves_per_eu(BOUNCE ? MYRT_BOUNCE_WPE : MYRT_MEGA_WPE)))
+#define MYRT_MEGA_ATTR \
+    __attribute__((amdgpu_waves_per_eu(BOUNCE ? MYRT_BOUNCE_WPE : QUEUE ? MYRT_QPRIM_WPE : MYRT_MEGA_WPE)))
 #else
 #define MYRT_MEGA_ATTR
 #endif
@@ -376,7 +374,8 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                 // walks; the memory clobber makes the reloads real loads.
                 if (!BOUNCE) pacc[3 * 64] = __builtin_bit_cast(double, rng.state);
                 const V3 col = trace_path<COUNT, BOUNCE, UNI, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt,
-                                                                     pacc + 3 * 64, i, j, &deferred);
+                                                                     pacc + 3 * 64, i, j, &deferred,
+                                                                     tile * wpb + wave);
                 asm volatile("" ::: "memory");
                 if (!BOUNCE) {
                     rng.state = __builtin_bit_cast(unsigned long long, (double)pacc[3 * 64]);
@@ -466,11 +465,64 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 
 namespace myrt {
 namespace dev {
-// One level of the compacted bounce render: the rays trace(depth = level) of every queued
-// sample, one lane per ray, waves taking 64 records at a time from the level's queue.
-// A mirror/conductor hit below maxRecursionDepth queues level + 1 (its own Lo follows after
-// the shadow walks); any other end resolves the sample backward through the records of its
-// ancestors and stores the pixel.  The last level's last wave zeroes the queue words.
+// Per level: the tiles with rays at `level` (their mask is non-zero) and the exclusive prefix of
+// their ray counts, in tile order; totals to the counters.  One block (a few microseconds).
+__global__ __launch_bounds__(1024) void k_qscan(RenderParams P, int level) {
+    __shared__ unsigned s_rays[1024], s_tiles[1024];
+    const int t = threadIdx.x, n = P.bounce_tiles;
+    const unsigned long long* m = P.bmask + (size_t)(level - 1) * n;
+    const int per = (n + 1023) / 1024;
+    const int b = min(n, t * per), e = min(n, b + per);
+    unsigned rays = 0, tiles = 0;
+    for (int k = b; k < e; ++k) {
+        const unsigned c = (unsigned)__popcll(m[k]);
+        rays += c;
+        tiles += c ? 1u : 0u;
+    }
+    s_rays[t] = rays; s_tiles[t] = tiles;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {                        // inclusive scans
+        const unsigned r = t >= off ? s_rays[t - off] : 0u, q = t >= off ? s_tiles[t - off] : 0u;
+        __syncthreads();
+        s_rays[t] += r; s_tiles[t] += q;
+        __syncthreads();
+    }
+    unsigned run = s_rays[t] - rays, at = s_tiles[t] - tiles;
+    for (int k = b; k < e; ++k) {
+        const unsigned c = (unsigned)__popcll(m[k]);
+        if (c) {
+            P.bact[at] = (uint32_t)k;
+            P.bact[n + at] = run;
+            ++at;
+            run += c;
+        }
+    }
+    if (t == 1023) {
+        P.counters[kQueueCount + level] = s_rays[1023];
+        P.counters[kQueueTiles + level] = s_tiles[1023];
+    }
+}
+
+// Position of the r-th set bit (r < popcount(m)).
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned r) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const unsigned lo = (unsigned)__popcll(m & ((1ull << w) - 1ull));
+        if (r >= lo) { r -= lo; m >>= w; pos += w; }
+    }
+    return pos;
+}
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long x, int src) {
+    const unsigned lo = (unsigned)__shfl((int)(unsigned)x, src, 64), hi = (unsigned)__shfl((int)(unsigned)(x >> 32), src, 64);
+    return (unsigned long long)lo | ((unsigned long long)hi << 32);
+}
+
+// One level of the compacted bounce render: the rays trace(depth = level), one lane per ray;
+// wave w of the grid takes the batches of 64 consecutive rays (tile order) w, w + G, ...
+// A mirror/conductor hit below maxRecursionDepth writes its pixel's level + 1 record (its own
+// Lo follows after the shadow walks) and sets its bit in the tile's next-level mask; any other
+// end resolves the sample backward through its pixel's records and stores the pixel.
 #ifndef MYRT_QUEUE_WPE
 #define MYRT_QUEUE_WPE 4
 #endif
@@ -480,18 +532,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
     extern __shared__ unsigned long long lds_stack[];
     const int lane = threadIdx.x & 63;
     Counts cnt{};
-    const unsigned long long n =
-        __hip_atomic_load(&P.counters[kQueueCount + level], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const long long lbase = (long long)(level - 1) * P.bounce_cap;
+    const unsigned T = (unsigned)P.counters[kQueueCount + level];     // written by k_qscan (previous launch)
+    const unsigned A = (unsigned)P.counters[kQueueTiles + level];
+    const int ntiles = P.bounce_tiles;
+    const uint32_t* atile = P.bact;
+    const uint32_t* apre = P.bact + ntiles;
+    const unsigned long long* mask = P.bmask + (size_t)(level - 1) * ntiles;
     MYRT_STACK(st, lds_stack);
     st.uni_spill = true;
-    for (;;) {
-        unsigned base = 0;
-        if (lane == 0) base = (unsigned)atomicAdd(&P.counters[kQueueGrab + level], 64ull);
-        base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
-        if (base >= n) break;
-        if (base + lane >= n) continue;
-        const long long g = lbase + base + lane;
+    for (unsigned x0 = blockIdx.x * 64u; x0 < T; x0 += gridDim.x * 64u) {
+        // the batch's first tile: the last active tile whose prefix is <= x0 (64-way search)
+        unsigned lo = 0, hi = A;                        // apre[lo] <= x0 < apre[hi] (apre[A] = T)
+        while (hi - lo > 1) {
+            const unsigned pos = lo + (unsigned)(((unsigned long long)(hi - lo) * (unsigned)lane) >> 6);
+            const unsigned long long le = __ballot(apre[pos] <= x0);
+            const int last = 63 - __builtin_clzll(le);
+            const unsigned nlo = (unsigned)__builtin_amdgcn_readlane((int)pos, last);
+            hi = last < 63 ? (unsigned)__builtin_amdgcn_readlane((int)pos, last + 1) : hi;
+            lo = nlo;
+        }
+        // the batch spans at most 64 active tiles from there: lane l holds tile lo + l
+        const unsigned a = lo + (unsigned)lane;
+        const bool in = a < A;
+        const unsigned pre = in ? apre[a] : 0xffffffffu;
+        const unsigned tl = in ? atile[a] : 0u;
+        const unsigned long long mk = in ? mask[tl] : 0ull;
+        const unsigned b = x0 + (unsigned)lane;          // this lane's ray
+        int jl = 0, jh = 64;                             // its tile: the last lane with pre <= b
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            const int mid = (jl + jh) >> 1;
+            if ((unsigned)__shfl((int)pre, mid, 64) <= b) jl = mid; else jh = mid;
+        }
+        const unsigned rank = b - (unsigned)__shfl((int)pre, jl, 64);
+        const unsigned long long myMask = shfl_u64(mk, jl);
+        const unsigned myTile = (unsigned)__shfl((int)tl, jl, 64);
+        if (b >= T) continue;
+        const int bit = nth_set_bit(myMask, rank);
+        const long long slot = (long long)myTile * 64 + bit;
+        const long long g = (long long)(level - 1) * P.bounce_cap + slot;
         const BounceRec& R = P.bounce[g];
         const V3 o = ld3(R.o), d = ld3(R.d);
         const double time = UNI ? 0.0 : R.time;
@@ -516,16 +595,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
                 const bool computeDirect = !(M.ior > 0) || frontFacing;
                 V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
                 const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && level < P.max_depth;
-                const long long q = queue_reserve(P, level + 1, want);
-                if (q >= 0) {
+                const long long q = want ? (long long)level * P.bounce_cap + slot : -1ll;
+                if (want) {
                     const BounceRec& Rs = P.bounce[g];
                     PCG32 r = PCG32::resume(Rs.rng, pixel_seed(Rs.i, Rs.j));
-                    queue_write(P, q, M, d, N, p, r, Rs.time, Rs.i, Rs.j, (int)g);
+                    queue_write(P, q, M, d, N, p, r, Rs.time, Rs.i, Rs.j);
+                    atomicOr(&P.bmask[(size_t)level * ntiles + myTile], 1ull << bit);
                     cnt.secondary++;
                 }
                 auto none = []() {};
                 if (computeDirect) point_lights<false, UNI>(P, M, N, p, d, time, st, cnt, Lo, none, none);
-                if (q >= 0) {
+                if (want) {
                     queue_write_lo(P, q, Lo);
                     ends = false;
                 } else {
@@ -533,15 +613,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
                 }
             }
         }
-        if (ends) {      // back through the ancestors: Lo_k + M_k * L_(k+1), NaN guard per level
-            long long r = g;
+        if (ends) {      // back through the pixel's records: Lo_k + M_k * L_(k+1), NaN guard per level
             int pi = 0, pj = 0;
-            for (;;) {
-                const BounceRec& A = P.bounce[r];
-                const V3 Lo = ld3(A.Lo) + ld3(A.M) * L;
+            for (int lev = level; lev >= 1; --lev) {
+                const BounceRec& Q = P.bounce[(long long)(lev - 1) * P.bounce_cap + slot];
+                const V3 Lo = ld3(Q.Lo) + ld3(Q.M) * L;
                 L = isfin(Lo) ? Lo : v3(0, 0, 0);
-                if (A.parent < 0) { pi = A.i; pj = A.j; break; }
-                r = A.parent;
+                pi = Q.i; pj = Q.j;
             }
             const V3 pixel = v3(0.0 + L.x, 0.0 + L.y, 0.0 + L.z);   // the sample sum (one sample)
             store_pixel(P, pi, pj, pixel / (double)P.cam.samples);
@@ -553,13 +631,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
         if (s0) atomicAdd(&P.counters[0], s0);
         if (s1) atomicAdd(&P.counters[1], s1);
         if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
-        if (level == P.max_depth) {     // every wave of the last level is past its last grab
-            if (atomicAdd(&P.counters[kQueueDone], 1ull) == (unsigned long long)gridDim.x - 1)
-                for (int k = kQueueDone; k < kCounterWords; ++k) atomicExch(&P.counters[k], 0ull);
-        }
     }
 }
 
+// After the last level: tile masks and queue words back at zero for the next launch.
+__global__ void k_queue_reset(RenderParams P, int levels) {
+    const size_t n = (size_t)levels * P.bounce_tiles;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x)
+        P.bmask[k] = 0ull;
+    if (blockIdx.x == 0 && kQueueCount + (int)threadIdx.x < kCounterWords) P.counters[kQueueCount + threadIdx.x] = 0ull;
+}
 }  // namespace dev
 }  // namespace myrt
 
@@ -632,11 +713,14 @@ constexpr int kInFlight = RT_MAX_IN_FLIGHT;
 constexpr int kSubmitDmaDefault = 0;   // rt_render_submit delivery (MYRT_SUBMIT_DMA, submit_impl)
 // Queued bounce rays of one stream's renders (BounceRec, levels x records per level)
 struct BounceArena {
-    BounceRec* recs = nullptr;
-    int64_t cap = 0;                               // records allocated
+    void* base = nullptr;                          // records, tile masks, tile list (queue_arena)
+    int64_t levels = 0, tiles = 0;                 // capacity
 };
 // Compacted bounce render: device bytes one launch may take for its queues (else the megakernel)
 constexpr int64_t kQueueBytesCap = 16ll << 30;
+// Off by default: parity-green but slower than the bounce megakernel on C5 (DESIGN.md §4,
+// "Compacted bounce render"); MYRT_QUEUE=1 selects it.
+constexpr int32_t kQueueDefault = 0;
 struct Flight {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
@@ -726,7 +810,7 @@ static void free_replica(DeviceReplica& r) {
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart); (void)hipFree(r.wave_times);
     (void)hipFree(r.deep);
-    (void)hipFree(r.arena.recs);
+    (void)hipFree(r.arena.base);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.counters_ready) (void)hipEventDestroy(r.counters_ready);
@@ -740,7 +824,7 @@ static void free_replica(DeviceReplica& r) {
         (void)hipFree(f.counters);
         (void)hipFree(f.stage_rgb);
         (void)hipFree(f.stage_rgba);
-        (void)hipFree(f.arena.recs);
+        (void)hipFree(f.arena.base);
         if (f.host_counters) (void)hipHostFree(f.host_counters);
     }
     if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -753,13 +837,27 @@ static void free_replica(DeviceReplica& r) {
     r = DeviceReplica();
 }
 
+// Triangle arrays get one zeroed record past the end: a leaf walk may load the record after a
+// run's last triangle before it looks at `last` (device.h MYRT_LEAF_PREFETCH).
+template <class T>
+static int32_t upload_padded(const std::vector<T>& v, T** dst, int64_t& bytes) {
+    const size_t n = v.size() + 1;
+    HIP_TRY(hipMalloc((void**)dst, n * sizeof(T)));
+    HIP_TRY(hipMemset(*dst, 0, n * sizeof(T)));
+    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    bytes += (int64_t)(n * sizeof(T));
+    return RT_OK;
+}
+
 // Replica from another replica's device buffers: device-to-device over xGMI (or a local
 // copy when both live on one GPU) instead of a second PCIe upload from the host.
 template <class T>
-static int32_t replicate(const std::vector<T>& v, const T* src, int src_dev, T** dst, int dst_dev, int64_t& bytes) {
-    const size_t n = std::max<size_t>(1, v.size());
+static int32_t replicate(const std::vector<T>& v, const T* src, int src_dev, T** dst, int dst_dev, int64_t& bytes,
+                         bool padded = false) {
+    const size_t n = padded ? v.size() + 1 : std::max<size_t>(1, v.size());
     HIP_TRY(hipMalloc((void**)dst, n * sizeof(T)));
-    if (!v.empty()) HIP_TRY(hipMemcpyPeer(*dst, dst_dev, src, src_dev, v.size() * sizeof(T)));
+    if (padded) HIP_TRY(hipMemcpyPeer(*dst, dst_dev, src, src_dev, n * sizeof(T)));   // the zeroed record too
+    else if (!v.empty()) HIP_TRY(hipMemcpyPeer(*dst, dst_dev, src, src_dev, v.size() * sizeof(T)));
     bytes += (int64_t)(n * sizeof(T));
     return RT_OK;
 }
@@ -772,14 +870,14 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
         const int sd = src->device;
         if ((rc = replicate(S.recs, src->recs, sd, &r.recs, device, r.bytes)) != RT_OK) return rc;
         if ((rc = replicate(S.crecs, src->crecs, sd, &r.crecs, device, r.bytes)) != RT_OK) return rc;
-        if ((rc = replicate(S.ctris, src->ctris, sd, &r.ctris, device, r.bytes)) != RT_OK) return rc;
-        if ((rc = replicate(S.tris, src->tris, sd, &r.tris, device, r.bytes)) != RT_OK) return rc;
+        if ((rc = replicate(S.ctris, src->ctris, sd, &r.ctris, device, r.bytes, true)) != RT_OK) return rc;
+        if ((rc = replicate(S.tris, src->tris, sd, &r.tris, device, r.bytes, true)) != RT_OK) return rc;
         if ((rc = replicate(S.normals, src->normals, sd, &r.normals, device, r.bytes)) != RT_OK) return rc;
     } else {
         if ((rc = upload(S.recs, &r.recs, r.bytes)) != RT_OK) return rc;
         if ((rc = upload(S.crecs, &r.crecs, r.bytes)) != RT_OK) return rc;
-        if ((rc = upload(S.ctris, &r.ctris, r.bytes)) != RT_OK) return rc;
-        if ((rc = upload(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload_padded(S.ctris, &r.ctris, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload_padded(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
         if ((rc = upload(S.normals, &r.normals, r.bytes)) != RT_OK) return rc;
     }
     if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
@@ -1070,26 +1168,41 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
 
 // Compacted bounce render for this launch (render.hip k_bounce): mirror/conductor scenes whose
 // pixels trace one sample (Int(sqrt(spp)) == 1) with maxRecursionDepth <= kMaxQueueLevels;
-// `arena` grows to levels x pixels records (false: allocation refused or failed -> megakernel).
-static bool queue_arena(DeviceReplica& r, BounceArena* arena, RenderParams& P) {
-    if (!arena || env_int("MYRT_QUEUE", 0, 0, 1) == 0) return false;
+// `arena` grows to levels x (tiles x 64) records, the tile masks and k_qscan's tile list
+// (false: allocation refused or failed -> the bounce megakernel).
+static bool queue_arena(BounceArena* arena, RenderParams& P, int64_t tiles) {
+    if (!arena || env_int("MYRT_QUEUE", kQueueDefault, 0, 1) == 0) return false;
     if (P.cam.n != 1 || P.max_depth < 1 || P.max_depth > kMaxQueueLevels) return false;
-    const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;      // one ray per pixel and level at most
-    const int64_t need = px * P.max_depth;
-    if (need * (int64_t)sizeof(BounceRec) > kQueueBytesCap) return false;
-    if (need > arena->cap) {
-        (void)hipFree(arena->recs);
-        arena->recs = nullptr;
-        arena->cap = 0;
-        if (hipMalloc((void**)&arena->recs, (size_t)need * sizeof(BounceRec)) != hipSuccess) {
+    const int64_t levels = P.max_depth;
+    // sections at offsets fixed by the allocation's capacity: the tile masks stay where the
+    // previous launch (whatever its size) zeroed them
+    auto bytes = [](int64_t lv, int64_t tl) {
+        return (size_t)(lv * tl * 64) * sizeof(BounceRec) + (size_t)(lv * tl) * sizeof(unsigned long long) +
+               (size_t)(2 * tl) * sizeof(uint32_t);
+    };
+    if (levels > arena->levels || tiles > arena->tiles) {
+        const int64_t lv = std::max(levels, arena->levels), tl = std::max(tiles, arena->tiles);
+        if ((int64_t)bytes(lv, tl) > kQueueBytesCap) return false;
+        (void)hipFree(arena->base);
+        arena->base = nullptr;
+        arena->levels = arena->tiles = 0;
+        if (hipMalloc(&arena->base, bytes(lv, tl)) != hipSuccess || hipMemset(arena->base, 0, bytes(lv, tl)) != hipSuccess) {
             (void)hipGetLastError();
-            arena->recs = nullptr;
+            (void)hipFree(arena->base);
+            arena->base = nullptr;
             return false;
         }
-        arena->cap = need;
+        arena->levels = lv;
+        arena->tiles = tl;
     }
-    P.bounce = arena->recs;
-    P.bounce_cap = px;
+    const size_t recBytes = (size_t)(arena->levels * arena->tiles * 64) * sizeof(BounceRec);
+    const size_t maskBytes = (size_t)(arena->levels * arena->tiles) * sizeof(unsigned long long);
+    char* b = static_cast<char*>(arena->base);
+    P.bounce = reinterpret_cast<BounceRec*>(b);
+    P.bmask = reinterpret_cast<unsigned long long*>(b + recBytes);
+    P.bact = reinterpret_cast<uint32_t*>(b + recBytes + maskBytes);
+    P.bounce_cap = tiles * 64;
+    P.bounce_tiles = (int32_t)tiles;
     return true;
 }
 
@@ -1117,17 +1230,19 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     const char* ue = std::getenv("MYRT_UNIFIED");
     const bool uni = P.identity && P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
 #define MYRT_LAUNCH(C_, B_, U_) hipLaunchKernelGGL((dev::render_kernel<C_, B_, U_>), grid, block, lds, stream, P)
-    if (bounce && !count && queue_arena(r, arena, P)) {
-        // primary + shadow rays of every pixel in the spill-free primary instantiation, then one
-        // k_bounce launch per level over the compacted queues
+    if (bounce && !count && queue_arena(arena, P, (int64_t)grid.x * (bt / 64))) {
+        // primary + shadow rays of every pixel in the spill-free primary instantiation, then per
+        // level the tile list (k_qscan) and the level's rays in coherent batches (k_bounce)
         if (uni) hipLaunchKernelGGL((dev::render_kernel<false, false, true, true>), grid, block, lds, stream, P);
         else hipLaunchKernelGGL((dev::render_kernel<false, false, false, true>), grid, block, lds, stream, P);
         const dim3 qgrid((unsigned)(r.cus * 4 * MYRT_QUEUE_WPE)), qblock(64);
         const size_t qlds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
         for (int32_t level = 1; level <= P.max_depth; ++level) {
+            hipLaunchKernelGGL(dev::k_qscan, dim3(1), dim3(1024), 0, stream, P, level);
             if (uni) hipLaunchKernelGGL((dev::k_bounce<true>), qgrid, qblock, qlds, stream, P, level);
             else hipLaunchKernelGGL((dev::k_bounce<false>), qgrid, qblock, qlds, stream, P, level);
         }
+        hipLaunchKernelGGL(dev::k_queue_reset, dim3(256), dim3(256), 0, stream, P, (int)P.max_depth);
     } else if (count) {
         if (bounce) { if (uni) MYRT_LAUNCH(true, true, true); else MYRT_LAUNCH(true, true, false); }
         else { if (uni) MYRT_LAUNCH(true, false, true); else MYRT_LAUNCH(true, false, false); }

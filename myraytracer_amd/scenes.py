@@ -19,7 +19,7 @@ from typing import Dict, Tuple
 
 import numpy as np
 
-from .scene import Camera, Material, Mesh, PointLight, Scene
+from .scene import AreaLight, Camera, Material, Mesh, MeshInstance, PointLight, Scene
 
 
 # ----------------------------------------------------------------------------- PLY
@@ -266,6 +266,72 @@ def scene_c5(path_dir: str = None, width: int = 3840, height: int = 2160, inline
                  near_distance=1.0, image_resolution=(width, height), image_name="c5.png")
     return Scene(cameras=[cam], materials=[_std_material((0.6, 0.7, 0.5)), _std_material((0.2, 0.2, 0.2), "mirror")],
                  objects=[terrain, mirrors], point_lights=[PointLight((40.0, 80.0, 60.0), (4.0e5, 4.0e5, 4.0e5))],
+                 ambient_light=(15.0, 15.0, 15.0), background_color=(40.0, 60.0, 90.0), shadow_ray_epsilon=1e-3,
+                 intersection_test_epsilon=1e-6, max_recursion_depth=4)
+
+
+def _placement(s: float, tx: float, ty: float, tz: float):
+    """Column-major localToWorld of a uniform scale s followed by a translation."""
+    return (s, 0.0, 0.0, 0.0, 0.0, s, 0.0, 0.0, 0.0, 0.0, s, 0.0, tx, ty, tz, 1.0)
+
+
+def scene_c3_instanced(path_dir: str = None, width: int = 1920, height: int = 1080, inline: bool = False) -> Scene:
+    """C3's geometry as mesh instances with non-identity transforms (the literal intersectTLAS
+    walk, RTContext.swift:619-720, every object an instance, :122-241, 384-401): the 512^2
+    terrain translated, one displaced level-5 icosphere base mesh placed by scale + translation,
+    and 23 MeshInstances of it placed the way C3 places its 24 spheres.  1,015,808 triangles
+    traced (524,288 + 24 x 20,480), 2 BLASes, a TLAS of 25 instances; same camera and light."""
+    seed = 42
+    hp, hf = heightfield(512, 100.0, 6.0, seed)
+    rng = np.random.RandomState(seed + 1)
+    Vs, Fs = icosphere(5)
+    Vb = _displace(Vs, 0.05, seed + 10)
+    places = []
+    for q in range(24):
+        r = rng.uniform(1.0, 3.0)
+        cx, cz = rng.uniform(-22, 22), rng.uniform(-22, 22)
+        places.append(_placement(r, cx, 5.0 + r, cz))
+    terrain = _ply_or_inline(path_dir, "c3i_terrain.ply", hp, hf, "smooth", 1, "1", inline)
+    terrain.transform = _placement(1.0, 0.0, -0.25, 0.0)
+    base = _ply_or_inline(path_dir, "c3i_icosphere.ply", Vb, Fs, "smooth", 2, "1", inline)
+    base.transform = places[0]
+    objs = [terrain, base] + [MeshInstance(id=3 + q, base_mesh_id=2, transform=places[q]) for q in range(1, 24)]
+    cam = Camera(position=(0.0, 18.0, 42.0), gaze_point=(0.0, 0.0, 8.0), up=(0.0, 1.0, 0.0), fovy=50.0,
+                 near_distance=1.0, image_resolution=(width, height), image_name="c3i.png")
+    return Scene(cameras=[cam], materials=[_std_material((0.6, 0.7, 0.5))], objects=objs,
+                 point_lights=[PointLight((30.0, 40.0, 40.0), (3.0e5, 3.0e5, 3.0e5))], ambient_light=(15.0, 15.0, 15.0),
+                 background_color=(40.0, 60.0, 90.0), shadow_ray_epsilon=1e-3, intersection_test_epsilon=1e-6,
+                 max_recursion_depth=4)
+
+
+def scene_c3_glass(path_dir: str = None, width: int = 1920, height: int = 1080, inline: bool = False) -> Scene:
+    """C3's geometry with the 24 spheres made of glass (dielectric with Beer absorption, two
+    child rays per bounce, Object+Extension.swift:207-251) and two area lights next to the
+    point light (:145-186, the chunk-sequential jitterIndex): the full trace() kernels
+    (render_full, k_events + k_jscan).  Terrain and spheres are two meshes, maxRecursionDepth 4."""
+    seed = 42
+    hp, hf = heightfield(512, 100.0, 6.0, seed)
+    rng = np.random.RandomState(seed + 1)
+    Vs, Fs = icosphere(5)
+    parts = []
+    for q in range(24):
+        r = rng.uniform(1.0, 3.0)
+        cx, cz = rng.uniform(-22, 22), rng.uniform(-22, 22)
+        parts.append((_displace(Vs, 0.05, seed + 10 + q) * r + np.array([cx, 5.0 + r, cz]), Fs))
+    sp, sf = _merge(parts)
+    terrain = _ply_or_inline(path_dir, "c3g_terrain.ply", hp, hf, "smooth", 1, "1", inline)
+    glass = _ply_or_inline(path_dir, "c3g_spheres.ply", sp, sf, "smooth", 2, "2", inline)
+    cam = Camera(position=(0.0, 18.0, 42.0), gaze_point=(0.0, 0.0, 8.0), up=(0.0, 1.0, 0.0), fovy=50.0,
+                 near_distance=1.0, image_resolution=(width, height), image_name="c3g.png")
+    mats = [_std_material((0.6, 0.7, 0.5)),
+            Material(ambient=(0.0, 0.0, 0.0), diffuse=(0.05, 0.05, 0.05), specular=(0.5, 0.5, 0.5), phong=60.0,
+                     ior=1.5, absorption=(0.02, 0.04, 0.08), type="dielectric")]
+    return Scene(cameras=[cam], materials=mats, objects=[terrain, glass],
+                 point_lights=[PointLight((30.0, 40.0, 40.0), (3.0e5, 3.0e5, 3.0e5))],
+                 area_lights=[AreaLight(position=(-20.0, 30.0, 10.0), normal=(0.5, -1.0, -0.2), radiance=(900.0, 850.0, 800.0),
+                                        size=4.0),
+                              AreaLight(position=(25.0, 20.0, -10.0), normal=(-1.0, -0.6, 0.3),
+                                        radiance=(300.0, 400.0, 600.0), size=3.0)],
                  ambient_light=(15.0, 15.0, 15.0), background_color=(40.0, 60.0, 90.0), shadow_ray_epsilon=1e-3,
                  intersection_test_epsilon=1e-6, max_recursion_depth=4)
 

@@ -188,3 +188,29 @@ def test_concurrent_waits_on_one_ticket():
         assert oks[0].shadow_rays == want.shadow_rays
         assert [r for k, r in res if k == "err"] == [A.RT_ERR_INVALID_ARG]
     eng.close()
+
+
+@pytest.mark.parametrize("queue", ["0", "1"])
+def test_pipelined_mirror_frames_against_the_oracle(monkeypatch, queue):
+    """Mirror frames in flight (each slot has its own bounce queues and counters): every frame
+    equals the oracle and carries the oracle's secondary-ray count."""
+    monkeypatch.setenv("MYRT_QUEUE", queue)
+    from test_gpu_features import _mirror_corridor
+    sc = _mirror_corridor(6, 80, 56)
+    ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
+    eng = M.RayTracerEngine(sc)
+    Q = A.RT_MAX_IN_FLIGHT
+    fbs = [M.pinned_array((56, 80, 4), np.uint8) for _ in range(Q)]
+    pend = []
+    for k in range(2 * Q + 3):
+        if len(pend) == Q:
+            kk, t = pend.pop(0)
+            st = eng.wait(t)
+            assert np.array_equal(fbs[kk % Q], ref8)
+            assert (st.shadow_rays, st.secondary_rays) == (ost.shadow_rays, ost.secondary_rays)
+        fbs[k % Q].fill(0)
+        pend.append((k, eng.submit_into(0, 0, 1, rgba=fbs[k % Q], frame_layout=True)))
+    for kk, t in pend:
+        eng.wait(t)
+        assert np.array_equal(fbs[kk % Q], ref8)
+    eng.close()

@@ -247,3 +247,41 @@ def test_deep_recursion_refused_past_the_buffer(monkeypatch):
         eng.render(0)
     assert e.value.code == A.RT_ERR_UNSUPPORTED
     eng.close()
+
+
+# ------------------------------------------------ compacted bounce render (render.hip k_bounce)
+def _rough_mirror_scene(w=128, h=96):
+    sc = _primitives_scene(w, h)
+    sc.materials.append(M.Material(ambient=(0.05, 0.05, 0.05), diffuse=(0.2, 0.2, 0.2), specular=(0.5, 0.5, 0.5),
+                                   phong=40.0, mirror=(0.8, 0.8, 0.8), roughness=0.05, type="mirror"))
+    sc.objects[3].material = "6"                       # rough mirror: PCG32 draws per bounce level
+    return sc
+
+
+@pytest.mark.parametrize("queue", ["0", "1"])
+def test_queued_bounces_against_the_oracle(monkeypatch, queue):
+    """Mirror/conductor scenes through the compacted bounce render (MYRT_QUEUE=1, the default:
+    primary pass + one k_bounce launch per level, rays resolved backward through their queue
+    records) and through the bounce megakernel (0): both equal the oracle's recursion
+    (Object+Extension.swift:189-206, 252-283).  Covers the general walk (a transformed
+    instance), rough mirrors, spp 3 (one traced sample divided by 3), the unified walk with 15
+    queue levels, chunk selections, and several replicas."""
+    monkeypatch.setenv("MYRT_QUEUE", queue)
+    sc = _rough_mirror_scene()
+    st = _compare(sc)
+    assert st.secondary_rays > 0
+    sc.cameras[0].num_samples = 3
+    _compare(sc)
+    st = _compare(_mirror_corridor(15, 48, 36))
+    assert st.secondary_rays > 10 * 48 * 36 // 2
+    _compare(_mirror_corridor(12, 48, 36), chunk_first=1, chunk_step=3)
+    # 3 chunks -> rt_render_ex's two staged launches of different sizes share one queue arena
+    _compare(_mirror_corridor(8, 64, 40), chunk_first=0, chunk_step=2)
+    sc = _mirror_corridor(8, 56, 40)
+    ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
+    eng = M.RayTracerEngine(sc, devices=[0, 0, 0])
+    for _ in range(2):                                 # queue words must be back at zero
+        rgb, rgba, st = eng.render_rows(0, 0, 1, True)
+        assert float(np.abs(rgb - ref).max()) <= TOL and np.array_equal(rgba, ref8)
+        assert st.secondary_rays == ost.secondary_rays
+    eng.close()

@@ -222,3 +222,28 @@ def test_bench_strong_split_eight_ranks_on_one_gpu():
     pr = eight["per_rank"]
     assert len(pr["ms_per_step"]) == 8 and pr["max_ms"] >= pr["min_ms"] > 0
     assert sum(pr["rows"]) == 600 and all(x > 0 for x in pr["submit_us_per_frame"])
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("name", ["c3i", "c3g"])
+def test_general_path_bench_configs_full_frame(scene_dir, name, monkeypatch):
+    """The bench's general-path configs on full 1920x1080 frames against the oracle: C3i (C3's
+    geometry as 25 transformed mesh instances: the literal TLAS->BLAS walk, RTContext.swift:
+    619-720) and C3g (glass spheres + two area lights: render_full with k_events/k_jscan,
+    Object+Extension.swift:145-251), through bench.py's call (RGBA8 into page-locked memory)
+    and the FP64 frame."""
+    monkeypatch.delenv("MYRT_PATH", raising=False)
+    make = {"c3i": scenes.scene_c3_instanced, "c3g": scenes.scene_c3_glass}[name]
+    sc = make(path_dir=scene_dir)
+    ref, ref8, ost = oracle.OracleScene(_inline(sc)).render(0, threads=0, rgba=True)
+    eng = M.RayTracerEngine(sc)
+    H, W = ref.shape[:2]
+    rgba = M.pinned_array((H, W, 4), np.uint8)
+    rgba.fill(0)
+    st = eng.render_into(0, 0, 1, rgb=None, rgba=rgba, frame_layout=True)
+    _assert_frame(None, rgba, ref, ref8)
+    assert (st.primary_rays, st.shadow_rays, st.secondary_rays) == \
+        (ost.primary_rays, ost.shadow_rays, ost.secondary_rays)
+    rgb, _, _ = eng.render_rows(0, 0, 1, False)
+    _assert_frame(rgb, None, ref, ref8)
+    eng.close()

@@ -17,7 +17,7 @@ eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
 stream = torch.cuda.current_stream()
 out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
-KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI")
+KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE")
 
 
 def t_frame(k=20):
@@ -40,4 +40,8 @@ for rep in range(2):
         for kv in combo.split():
             k, v = kv.split("=")
             os.environ[k] = v
-        print(f"{cfg} [{combo}] {t_frame():.4f} ms", flush=True)
+        ms = t_frame()
+        import hashlib
+        sha = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
+        print(f"{cfg} [{combo}] {ms:.4f} ms  frame sha1 {sha}  secondary {eng.collect_stats().secondary_rays}",
+              flush=True)
