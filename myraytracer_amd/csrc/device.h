@@ -810,6 +810,137 @@ __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o,
     return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);
 }
 
+// Walks of the render kernels (render.hip WALK template argument)
+constexpr int kWalkGeneral = 0, kWalkIdentity = 1, kWalkTransformed = 2;
+
+// ------------------------------------------------------- unified transformed walk (UT)
+// Scenes whose instances carry transforms or motion (every object of a reference scene is an
+// instance, RTContext.swift:122-241, 384-401).  intersect_closest/occluded nest a BLAS walk
+// inside the TLAS walk, so the lanes of a wave sit in different loop nests and run them one
+// after the other.  Here TLAS and BLAS records are walked in ONE loop with one stack: a TLAS
+// leaf pushes a marker per instance (in reverse, so they pop in leaf order); popping a marker
+// switches the lane's ray to that instance's local ray - the same world->local arithmetic as
+// intersectTLAS (:655-673) - and tests the instance's BLAS root (intersectBLAS's first pop,
+// :567-571); a popped TLAS entry switches back to the world ray.  Each BLAS is finished before
+// the next marker pops, so instances and their nodes are visited in intersectTLAS's order
+// (near child first, ties to L, :641-706): hits - including equal-t ties - are the reference's.
+// Stack bound: TLAS path + the largest TLAS leaf + BLAS path (HostScene::max_stack_unified).
+struct UtRay {
+    V3 o, d, inv;      // the current ray (world, or instance `inst`'s local ray)
+    int inst;          // -1 = world
+    bool fast;         // every 1/d component finite (slab_hit<true> allowed)
+};
+// back to the world ray; 1/d is recomputed (the same IEEE divisions as the caller's) rather than
+// kept live across the walk
+__device__ __forceinline__ void ut_world(UtRay& R, const V3& o, const V3& d) {
+    R.o = o; R.d = d; R.inv = rcp(d); R.inst = -1; R.fast = finite3(R.inv);
+}
+__device__ __forceinline__ void ut_local(const RenderParams& P, UtRay& R, int k, const V3& o, const V3& d,
+                                         double time) {
+    const DInstance& I = P.insts[k];
+    const V3 instOffset = ld3(I.motion) * time;
+    R.o = m4_point(I.w2l, o - instOffset, 1.0);
+    R.d = m4_point(I.w2l, d, 0.0);
+    R.inv = rcp(R.d);
+    R.inst = k;
+    R.fast = finite3(R.inv);
+}
+__device__ __forceinline__ bool ut_is_marker(const RenderParams& P, int ref) { return ref < 0 && ~ref >= P.ut_marker_base; }
+__device__ __forceinline__ bool ut_is_tlas(const RenderParams& P, int ref) {
+    return ref >= 0 ? ref >= P.tlas_rec_base : (~ref >= P.tlas_leaf_base);
+}
+
+// Pop the next node to visit.  Markers switch the ray to their instance and test its BLAS root
+// (a sphere/plane instance's primitive is tested right there, `prim`); TLAS entries bring the
+// world ray back.  Returns 0 = `ref` holds the next node, 1 = stack exhausted, 2 = occluded
+// (SHADOW: a sphere/plane instance's primitive blocks the ray).
+template <bool SHADOW, class Prim>
+__device__ __forceinline__ int ut_pop(const RenderParams& P, Stack& st, int base, double lim, int& ref, UtRay& R,
+                                      const V3& o, const V3& d, double time, Prim prim) {
+    while (st.sp > base) {
+        double tlo;
+        const int r = st.pop(tlo);
+        if (ut_is_marker(P, r)) {
+            const int k = ~r - P.ut_marker_base;
+            ut_local(P, R, k, o, d, time);
+            const DInstance& I = P.insts[k];
+            double dr;
+            if (!slab_hit<false>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1], I.root_hi[2],
+                                 R.o, R.inv, P.eps, dr) || dr > lim)
+                continue;
+            if (I.kind != kPrimTriangles) {            // single-primitive BLAS (RTContext.swift:122-192)
+                if (prim(I, k)) return 2;
+                continue;
+            }
+            ref = I.root_ref;
+            return 0;
+        }
+        if (tlo > lim) continue;
+        if (R.inst >= 0 && ut_is_tlas(P, r)) ut_world(R, o, d);
+        ref = r;
+        return 0;
+    }
+    return 1;
+}
+
+// Closest hit (intersectTLAS) or any hit (occludedTLAS, order-free) of one world ray.
+// Returns the occlusion for SHADOW.
+template <bool SHADOW>
+__device__ __forceinline__ bool ut_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
+                                        double tmax, double time, Hit& h, Stack& st) {
+    Counts c{};
+    const double eps = P.eps;
+    const int base = st.sp;
+    UtRay R;
+    R.o = o; R.d = d; R.inv = inv; R.inst = -1; R.fast = finite3(inv);
+    int ref;
+    if (!unified_begin(P, o, inv, SHADOW ? tmax * P.prune_rel + P.prune_abs : DINF, ref)) return false;
+    bool occ = false;
+    auto prim = [&](const DInstance& I, int k) -> bool {
+        const TriRec& T = P.tris[~I.root_ref];
+        if (SHADOW) return prim_shadow(I.kind, T, R.o, R.d, tmax, eps);
+        double ht = h.t;
+        if (prim_closest(I.kind, T, R.o, R.d, tlo, eps, ht)) { h.t = ht; h.tri = ~I.root_ref; h.inst = k; }
+        return false;
+    };
+    for (;;) {
+        const double lim = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+        bool stepped = false;
+        if (ref >= 0) {                                       // TLAS or BLAS inner record
+            stepped = __all(R.fast) ? inner_step<false, true, SHADOW>(P, ref, R.o, R.inv, lim, st, c)
+                                    : inner_step<false, false, SHADOW>(P, ref, R.o, R.inv, lim, st, c);
+        } else if (~ref < P.tlas_leaf_base) {                 // BLAS leaf run, instance R.inst
+            // local origin minus the mesh's triangle motion (intersectTriangle :480-481)
+            const V3 omb = R.o - ld3(P.insts[R.inst].tri_motion) * time;
+            auto run = [&](const auto* tris) -> bool {
+                for (int t = ~ref;; ++t) {
+                    const auto T = tris[t];
+                    if (SHADOW) {
+                        if (tri_shadow(T, omb, R.d, 0.0, tmax, eps, P.fast_rcp)) return true;
+                    } else {
+                        tri_closest(T, omb, R.d, tlo, eps, h, t, R.inst, P.fast_rcp);
+                    }
+                    if (T.last) break;
+                }
+                return false;
+            };
+            if (P.ctris ? run(P.ctris) : run(P.tris)) { occ = true; break; }
+        } else {                                              // TLAS leaf: one marker per instance
+            const int k0 = ~ref - P.tlas_leaf_base;
+            int k1 = k0;
+            while (!P.tlas_leaf[k1].last) ++k1;
+            for (int k = k1; k >= k0; --k) st.push(~(P.ut_marker_base + P.tlas_leaf[k].inst), 0.0);
+        }
+        if (stepped) continue;
+        const double lim2 = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+        const int pr = ut_pop<SHADOW>(P, st, base, lim2, ref, R, o, d, time, prim);
+        if (pr == 2) { occ = true; break; }
+        if (pr == 1) break;
+    }
+    st.reset(base);
+    return occ;
+}
+
 // The hit record intersectTriangle/Sphere/Plane + intersectTLAS leave behind
 // (RTContext.swift:479-538, 674-705), rebuilt once for the final (t, tri, u, v, inst):
 // world hit point and the normalized, det-signed world geometric normal.

@@ -132,6 +132,9 @@ struct RenderParams {
     int32_t has_tlas;
     int32_t tlas_leaf_base;          // TriRec count: ~ref >= base means a TLAS leaf
     int32_t identity;                // unified TLAS+BLAS walk allowed (scene.h HostScene::identity)
+    int32_t ut;                      // unified transformed walk allowed (device.h ut_walk; stack bound)
+    int32_t tlas_rec_base;           // records [tlas_rec_base, ...) are TLAS records (ut_walk)
+    int32_t ut_marker_base;          // leaf refs ~e with e >= this are instance markers (ut_walk)
     int32_t num_mats;
     int32_t num_plights;
     DCamera cam;

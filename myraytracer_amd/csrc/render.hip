@@ -38,11 +38,38 @@ __device__ __forceinline__ unsigned long long pixel_seed(int i, int j) {
     return (((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull;
 }
 
+// Closest hit of one ray by the scene's walk (WALK, render_kernel).
+template <bool COUNT, int WALK>
+__device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
+                                             double time, Hit& h, Stack& st, Counts& c) {
+    if (WALK == kWalkIdentity) {
+        uni_closest<COUNT>(P, o, d, inv, tlo, h, st, c);
+    } else if (WALK == kWalkTransformed) {
+        h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+        (void)ut_walk<false>(P, o, d, inv, tlo, DINF, time, h, st);
+    } else {
+        intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
+    }
+}
+
+// Any hit of one shadow ray (tMin 0, tMax) by the scene's walk.
+template <bool COUNT, int WALK>
+__device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time,
+                                              Stack& st, Counts& c) {
+    if (WALK == kWalkIdentity) return uni_occluded<COUNT>(P, o, d, tmax, st, c);
+    if (WALK == kWalkTransformed) {
+        if (!P.has_tlas) return false;
+        Hit hu;
+        return ut_walk<true>(P, o, d, rcp(d), 0.0, tmax, time, hu, st);
+    }
+    return occluded<COUNT>(P, o, d, tmax, time, st, c);
+}
+
 // Point lights at a hit (Object+Extension.swift:116-143): adds the unoccluded Blinn-Phong
 // terms to Lo.  With !(N.L > 0) the reference discards the occlusion result, so that walk is
 // skipped; the ray is still counted as cast.
 // park/unpark: the caller's PCG32 state moves to LDS around each walk (trace_path BOUNCE).
-template <bool COUNT, bool UNI, class Park, class Unpark>
+template <bool COUNT, int WALK, class Park, class Unpark>
 __device__ __forceinline__ void point_lights(const RenderParams& P, const DMaterial& M, const V3& N, const V3& p,
                                              const V3& d, double time, Stack& st, Counts& c, V3& Lo, Park park,
                                              Unpark unpark) {
@@ -73,8 +100,7 @@ __device__ __forceinline__ void point_lights(const RenderParams& P, const DMater
         if (NdotL > 0 || MYRT_REF(P)) {
             c.shadow_traced++;
             park();
-            const bool blocked = UNI ? uni_occluded<COUNT>(P, so, wi, dist, st, c)
-                                     : occluded<COUNT>(P, so, wi, dist, time, st, c);
+            const bool blocked = walk_occluded<COUNT, WALK>(P, so, wi, dist, time, st, c);
             unpark();
             if (!blocked && NdotL > 0) Lo = Lo + contrib;
         }
@@ -154,7 +180,7 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, int i, int j,
 // its reflected ray to its pixel's level-1 record (slot `qtile * 64 + lane`, qtile = this wave's
 // tile) and sets `deferred`; k_bounce delivers that pixel.  The PCG32 state is read from
 // rng_slot (the caller parks it there) and (i, j) give its stream.
-template <bool COUNT, bool BOUNCE, bool UNI, bool QUEUE = false>
+template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
                          Counts& c, __attribute__((address_space(3))) double* rng_slot, int i = 0, int j = 0,
                          bool* deferred = nullptr, int qtile = 0) {
@@ -174,14 +200,13 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         const V3 inv = rcp(d);
         Hit h;
         park();
-        if (UNI) uni_closest<COUNT>(P, o, d, inv, tlo, h, st, c);
-        else intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
+        walk_closest<COUNT, WALK>(P, o, d, inv, tlo, time, h, st, c);
         unpark();
         if (h.inst < 0) { L = ld3(P.background); break; }
         V3 p, Ngeo;
         // identity scenes do not move (scene.cpp): motion*time == motion*0 for every time in
         // [0, 1), so `time` need not stay live across the walk
-        hit_geometry<COUNT>(P, o, d, UNI ? 0.0 : time, h, p, Ngeo, c);
+        hit_geometry<COUNT>(P, o, d, WALK == kWalkIdentity ? 0.0 : time, h, p, Ngeo, c);
         const DInstance& I = P.insts[h.inst];
         const int matIndex = max(0, min(P.num_mats - 1, I.material - 1));
         const DMaterial& M = P.mats[matIndex];
@@ -204,7 +229,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 }
             }
         }
-        if (computeDirect) point_lights<COUNT, UNI>(P, M, N, p, d, time, st, c, Lo, park, unpark);
+        if (computeDirect) point_lights<COUNT, WALK>(P, M, N, p, d, time, st, c, Lo, park, unpark);
         if (QUEUE && q >= 0) {
             queue_write_lo(P, q, Lo);
             *deferred = true;
@@ -284,10 +309,12 @@ typedef __attribute__((address_space(3))) double lds_f64;
 #include "render_full.h"
 namespace myrt {
 namespace dev {
-// UNI: identity scenes walk TLAS + BLAS as one tree (device.h unified_step).
+// WALK: kWalkIdentity = identity scenes walk TLAS + BLAS as one tree (device.h unified_step);
+// kWalkTransformed = the same with per-instance ray switches (device.h ut_walk); kWalkGeneral =
+// the nested TLAS/BLAS walks (intersect_closest / occluded; reference-order counting).
 // QUEUE: primary pass of the compacted bounce render (one traced sample per pixel, host-checked):
 // mirror/conductor hits queue their reflected rays and their pixels are stored by k_bounce.
-template <bool COUNT, bool BOUNCE, bool UNI, bool QUEUE = false>
+template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams P) {
     static_assert(!QUEUE || MYRT_PIXLDS, "the queued primary pass reads the PCG32 state from its LDS slot");
     extern __shared__ unsigned long long lds_stack[];
@@ -373,7 +400,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                 // in LDS while the rays are traced, so they are not live - spilled - across the
                 // walks; the memory clobber makes the reloads real loads.
                 if (!BOUNCE) pacc[3 * 64] = __builtin_bit_cast(double, rng.state);
-                const V3 col = trace_path<COUNT, BOUNCE, UNI, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt,
+                const V3 col = trace_path<COUNT, BOUNCE, WALK, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt,
                                                                      pacc + 3 * 64, i, j, &deferred,
                                                                      tile * wpb + wave);
                 asm volatile("" ::: "memory");
@@ -387,7 +414,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
                     pacc[0] = pacc[0] + col.x; pacc[64] = pacc[64] + col.y; pacc[128] = pacc[128] + col.z;
                 }
 #else
-                const V3 col = trace_path<COUNT, BOUNCE, UNI>(P, camEye, dir, tlo, time, rng, st, cnt, nullptr);
+                const V3 col = trace_path<COUNT, BOUNCE, WALK>(P, camEye, dir, tlo, time, rng, st, cnt, nullptr);
                 pixel = pixel + col;
 #endif
                 sampleIndex += 1;
@@ -526,7 +553,7 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long x, int
 #ifndef MYRT_QUEUE_WPE
 #define MYRT_QUEUE_WPE 4
 #endif
-template <bool UNI>
+template <int WALK>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_WPE))) void k_bounce(RenderParams P,
                                                                                                     int level) {
     extern __shared__ unsigned long long lds_stack[];
@@ -573,7 +600,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
         const long long g = (long long)(level - 1) * P.bounce_cap + slot;
         const BounceRec& R = P.bounce[g];
         const V3 o = ld3(R.o), d = ld3(R.d);
-        const double time = UNI ? 0.0 : R.time;
+        const double time = WALK == kWalkIdentity ? 0.0 : R.time;
         V3 L;
         bool ends = true;
         if (!P.has_tlas) {
@@ -581,8 +608,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
         } else {
             const V3 inv = rcp(d);
             Hit h;
-            if (UNI) uni_closest<false>(P, o, d, inv, 0.0, h, st, cnt);
-            else intersect_closest<false>(P, o, d, inv, 0.0, time, h, st, cnt);
+            walk_closest<false, WALK>(P, o, d, inv, 0.0, time, h, st, cnt);
             if (h.inst < 0) {
                 L = ld3(P.background);
             } else {
@@ -604,7 +630,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
                     cnt.secondary++;
                 }
                 auto none = []() {};
-                if (computeDirect) point_lights<false, UNI>(P, M, N, p, d, time, st, cnt, Lo, none, none);
+                if (computeDirect) point_lights<false, WALK>(P, M, N, p, d, time, st, cnt, Lo, none, none);
                 if (want) {
                     queue_write_lo(P, q, Lo);
                     ends = false;
@@ -666,7 +692,8 @@ __global__ __launch_bounds__(256) void k_trace_rays(RenderParams P, RayBatch B) 
     Hit h;
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     if (P.has_tlas) {
-        if (B.uni) uni_closest<false>(P, o, d, rcp(d), B.tlim[i], h, st, c);
+        if (B.uni == 1) uni_closest<false>(P, o, d, rcp(d), B.tlim[i], h, st, c);
+        else if (B.uni == 2) (void)ut_walk<false>(P, o, d, rcp(d), B.tlim[i], DINF, time, h, st);
         else intersect_closest<false>(P, o, d, rcp(d), B.tlim[i], time, h, st, c);
     }
     V3 p = v3(0, 0, 0), n = v3(0, 0, 0);
@@ -683,7 +710,9 @@ __global__ __launch_bounds__(256) void k_occluded_rays(RenderParams P, RayBatch 
     MYRT_STACK(st, lds_stack);
     Counts c{};
     const V3 o = v3(B.o[3 * i], B.o[3 * i + 1], B.o[3 * i + 2]), d = v3(B.d[3 * i], B.d[3 * i + 1], B.d[3 * i + 2]);
-    const bool hit = B.uni ? uni_occluded<false>(P, o, d, B.tlim[i], st, c)
+    Hit hu;
+    const bool hit = B.uni == 1 ? uni_occluded<false>(P, o, d, B.tlim[i], st, c)
+                     : B.uni == 2 ? (P.has_tlas && ut_walk<true>(P, o, d, rcp(d), 0.0, B.tlim[i], B.time[i], hu, st))
                            : occluded<false>(P, o, d, B.tlim[i], B.time[i], st, c);
     B.out_occ[i] = hit ? 1 : 0;
 }
@@ -1039,6 +1068,10 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.has_tlas = S.has_tlas ? 1 : 0;
     P.tlas_leaf_base = (int32_t)S.tlas_leaf_base;
     P.identity = S.identity ? 1 : 0;
+    // one stack for TLAS + BLAS + a TLAS leaf's markers (HostScene::max_stack_unified)
+    P.ut = (S.has_tlas && S.max_stack_unified <= kStackCap && env_int("MYRT_UT", 1, 0, 1) == 1) ? 1 : 0;
+    P.tlas_rec_base = (int32_t)S.blas_records;
+    P.ut_marker_base = (int32_t)(S.tlas_leaf_base + (int64_t)S.tlas_leaf.size());
     P.num_mats = (int32_t)S.mats.size();
     P.num_plights = (int32_t)S.plights.size();
     P.cam = camera_constants(S.cams[cam]);
@@ -1131,6 +1164,16 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
         }
         P.deep = r.deep;
     }
+    const char* ue = std::getenv("MYRT_UNIFIED");
+    const bool unified = P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
+    const int walk = (unified && P.identity) ? dev::kWalkIdentity
+                     : (unified && P.ut && !count) ? dev::kWalkTransformed : dev::kWalkGeneral;
+#define MYRT_BY_WALK(M_)                                                    \
+    do {                                                                    \
+        if (walk == dev::kWalkIdentity) M_(dev::kWalkIdentity);             \
+        else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
+        else M_(dev::kWalkGeneral);                                         \
+    } while (0)
     if (P.num_alights > 0) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
         if (px > r.cap_px) {
@@ -1146,22 +1189,37 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
         for (int32_t base = 0; base < P.num_chunks; base += batch) {
             P.slot_base = base;
             dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);
-            if (deep) hipLaunchKernelGGL((dev::k_events<true>), grid, block, lds, stream, P);
-            else hipLaunchKernelGGL((dev::k_events<false>), grid, block, lds, stream, P);
+#define MYRT_EV1(W_) hipLaunchKernelGGL((dev::k_events<true, W_>), grid, block, lds, stream, P)
+#define MYRT_EV0(W_) hipLaunchKernelGGL((dev::k_events<false, W_>), grid, block, lds, stream, P)
+            if (deep) MYRT_BY_WALK(MYRT_EV1);
+            else MYRT_BY_WALK(MYRT_EV0);
+#undef MYRT_EV1
+#undef MYRT_EV0
         }
         hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), dim3(256, 1, 1), 0, stream, P);
     }
     for (int32_t base = 0; base < P.num_chunks; base += batch) {
         P.slot_base = base;
         dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);
-        if (deep) {
-            if (count) hipLaunchKernelGGL((dev::render_full<true, true>), grid, block, lds, stream, P);
-            else hipLaunchKernelGGL((dev::render_full<false, true>), grid, block, lds, stream, P);
+        const bool u = walk == dev::kWalkIdentity;
+        if (count) {
+            if (deep) {
+                if (u) hipLaunchKernelGGL((dev::render_full<true, true, dev::kWalkIdentity>), grid, block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::render_full<true, true, dev::kWalkGeneral>), grid, block, lds, stream, P);
+            } else {
+                if (u) hipLaunchKernelGGL((dev::render_full<true, false, dev::kWalkIdentity>), grid, block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::render_full<true, false, dev::kWalkGeneral>), grid, block, lds, stream, P);
+            }
         } else {
-            if (count) hipLaunchKernelGGL((dev::render_full<true, false>), grid, block, lds, stream, P);
-            else hipLaunchKernelGGL((dev::render_full<false, false>), grid, block, lds, stream, P);
+#define MYRT_RF1(W_) hipLaunchKernelGGL((dev::render_full<false, true, W_>), grid, block, lds, stream, P)
+#define MYRT_RF0(W_) hipLaunchKernelGGL((dev::render_full<false, false, W_>), grid, block, lds, stream, P)
+            if (deep) MYRT_BY_WALK(MYRT_RF1);
+            else MYRT_BY_WALK(MYRT_RF0);
+#undef MYRT_RF1
+#undef MYRT_RF0
         }
     }
+#undef MYRT_BY_WALK
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -1226,30 +1284,48 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     dim3 block((unsigned)bt, 1, 1);
     const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long) + (size_t)dev::kPixSlots * bt * sizeof(double);
     const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
-    // the unified walk needs an identity scene; reference-order counting uses the general walk
+    // The walk: identity scenes walk TLAS + BLAS as one tree; other scenes the unified transformed
+    // walk (per-instance ray switches), or the nested general walk when the stack bound does not
+    // allow one stack or for counting launches (reference-order counting needs the general walk)
     const char* ue = std::getenv("MYRT_UNIFIED");
-    const bool uni = P.identity && P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
-#define MYRT_LAUNCH(C_, B_, U_) hipLaunchKernelGGL((dev::render_kernel<C_, B_, U_>), grid, block, lds, stream, P)
+    const bool unified = P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
+    const int walk = (unified && P.identity) ? dev::kWalkIdentity
+                     : (unified && P.ut && !count) ? dev::kWalkTransformed : dev::kWalkGeneral;
+#define MYRT_LAUNCH(C_, B_, W_) hipLaunchKernelGGL((dev::render_kernel<C_, B_, W_>), grid, block, lds, stream, P)
+#define MYRT_BY_WALK(M_)                                                    \
+    do {                                                                    \
+        if (walk == dev::kWalkIdentity) M_(dev::kWalkIdentity);             \
+        else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
+        else M_(dev::kWalkGeneral);                                         \
+    } while (0)
     if (bounce && !count && queue_arena(arena, P, (int64_t)grid.x * (bt / 64))) {
         // primary + shadow rays of every pixel in the spill-free primary instantiation, then per
         // level the tile list (k_qscan) and the level's rays in coherent batches (k_bounce)
-        if (uni) hipLaunchKernelGGL((dev::render_kernel<false, false, true, true>), grid, block, lds, stream, P);
-        else hipLaunchKernelGGL((dev::render_kernel<false, false, false, true>), grid, block, lds, stream, P);
+#define MYRT_QPRIM(W_) hipLaunchKernelGGL((dev::render_kernel<false, false, W_, true>), grid, block, lds, stream, P)
+        MYRT_BY_WALK(MYRT_QPRIM);
+#undef MYRT_QPRIM
         const dim3 qgrid((unsigned)(r.cus * 4 * MYRT_QUEUE_WPE)), qblock(64);
         const size_t qlds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
         for (int32_t level = 1; level <= P.max_depth; ++level) {
             hipLaunchKernelGGL(dev::k_qscan, dim3(1), dim3(1024), 0, stream, P, level);
-            if (uni) hipLaunchKernelGGL((dev::k_bounce<true>), qgrid, qblock, qlds, stream, P, level);
-            else hipLaunchKernelGGL((dev::k_bounce<false>), qgrid, qblock, qlds, stream, P, level);
+#define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), qgrid, qblock, qlds, stream, P, level)
+            MYRT_BY_WALK(MYRT_QB);
+#undef MYRT_QB
         }
         hipLaunchKernelGGL(dev::k_queue_reset, dim3(256), dim3(256), 0, stream, P, (int)P.max_depth);
     } else if (count) {
-        if (bounce) { if (uni) MYRT_LAUNCH(true, true, true); else MYRT_LAUNCH(true, true, false); }
-        else { if (uni) MYRT_LAUNCH(true, false, true); else MYRT_LAUNCH(true, false, false); }
+        const bool u = walk == dev::kWalkIdentity;
+        if (bounce) { if (u) MYRT_LAUNCH(true, true, dev::kWalkIdentity); else MYRT_LAUNCH(true, true, dev::kWalkGeneral); }
+        else { if (u) MYRT_LAUNCH(true, false, dev::kWalkIdentity); else MYRT_LAUNCH(true, false, dev::kWalkGeneral); }
     } else {
-        if (bounce) { if (uni) MYRT_LAUNCH(false, true, true); else MYRT_LAUNCH(false, true, false); }
-        else { if (uni) MYRT_LAUNCH(false, false, true); else MYRT_LAUNCH(false, false, false); }
+#define MYRT_B1(W_) MYRT_LAUNCH(false, true, W_)
+#define MYRT_B0(W_) MYRT_LAUNCH(false, false, W_)
+        if (bounce) MYRT_BY_WALK(MYRT_B1);
+        else MYRT_BY_WALK(MYRT_B0);
+#undef MYRT_B1
+#undef MYRT_B0
     }
+#undef MYRT_BY_WALK
 #undef MYRT_LAUNCH
     HIP_TRY(hipGetLastError());
     return RT_OK;
@@ -2057,7 +2133,8 @@ static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o,
     dev::RayBatch B{};
     B.n = n;
     const char* ue = std::getenv("MYRT_UNIFIED");
-    B.uni = (P.identity && P.has_tlas && !(ue && ue[0] == '0')) ? 1 : 0;
+    const bool unified = P.has_tlas && !(ue && ue[0] == '0');
+    B.uni = (unified && P.identity) ? 1 : (unified && P.ut) ? 2 : 0;   // the render kernels' walk
     std::vector<void*> allocs;
     auto dalloc = [&](size_t bytes, void** p) -> int32_t {
         HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 8)));

@@ -67,7 +67,7 @@ struct FrameStack {
     }
 };
 
-template <bool COUNT, bool EVENTS, bool DEEP>
+template <bool COUNT, bool EVENTS, bool DEEP, int WALK>
 __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng,
                          long long& jitterIndex, Stack& st, Counts& c) {
     FrameStack<DEEP> F;
@@ -86,7 +86,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
             out = LevelOut{v3(0, 0, 0), false, 0, DINF};
         } else {
             Hit h;
-            intersect_closest<COUNT>(P, o, d, rcp(d), tlo, time, h, st, c);
+            walk_closest<COUNT, WALK>(P, o, d, rcp(d), tlo, time, h, st, c);
             if (h.inst < 0) {                                        // :101-103
                 out = LevelOut{ld3(P.background), false, 0, DINF};
             } else {
@@ -110,7 +110,8 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                             const double NdotL = smax(0.0, dot(N, wi));
                             if (NdotL > 0 || MYRT_REF(P)) {                 // else the result is discarded
                                 c.shadow_traced++;
-                                const bool blocked = occluded<COUNT>(P, p + wi * P.shadow_eps, wi, dist, time, st, c);
+                                const bool blocked =
+                                    walk_occluded<COUNT, WALK>(P, p + wi * P.shadow_eps, wi, dist, time, st, c);
                                 if (!blocked && NdotL > 0) {
                                     const double shininess = smax(1.0, M.phong);
                                     const V3 Ld = ld3(M.diffuse) * NdotL;
@@ -147,7 +148,8 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                         if (Ln <= 0) continue;
                         c.shadow++;
                         c.shadow_traced++;
-                        if (occluded<COUNT>(P, p + wi * P.shadow_eps, wi, dist - P.shadow_eps, time, st, c)) continue;
+                        if (walk_occluded<COUNT, WALK>(P, p + wi * P.shadow_eps, wi, dist - P.shadow_eps, time, st, c))
+                            continue;
                         const V3 view = normalize(-d);
                         const V3 hv = normalize(wi + view);
                         const V3 Ld = ld3(M.diffuse) * NdotL;
@@ -261,7 +263,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
 }
 
 // Pixel loop shared by k_events and render_full (Object+Extension.swift:292-356).
-template <bool COUNT, bool EVENTS, bool DEEP>
+template <bool COUNT, bool EVENTS, bool DEEP, int WALK>
 __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, long long& jitterIndex, Stack& st,
                                          Counts& c) {
     const DCamera& C = P.cam;
@@ -294,7 +296,8 @@ __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, lo
             const double time = rng.nextFloat();
             const double denom = dot(dir, w);
             const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
-            pixel = pixel + trace_full<COUNT, EVENTS, DEEP>(P, camEye, dir, smax(tImg, 0.0), time, rng, jitterIndex, st, c);
+            pixel = pixel + trace_full<COUNT, EVENTS, DEEP, WALK>(P, camEye, dir, smax(tImg, 0.0), time, rng, jitterIndex,
+                                                                  st, c);
             sampleIndex += 1;
             if (sampleIndex >= C.samples) break;
         }
@@ -315,8 +318,16 @@ __device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int
 }
 
 // Pass 1: area-light evaluations per pixel of the selection (packed rows).
-template <bool DEEP>
-__global__ __launch_bounds__(256) void k_events(RenderParams P) {
+#ifndef MYRT_FULL_WPE
+#define MYRT_FULL_WPE 0      // waves/SIMD for render_full and k_events (0 = the compiler's choice)
+#endif
+#if MYRT_FULL_WPE > 0
+#define MYRT_FULL_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_FULL_WPE)))
+#else
+#define MYRT_FULL_ATTR
+#endif
+template <bool DEEP, int WALK>
+__global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_events(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
@@ -324,7 +335,7 @@ __global__ __launch_bounds__(256) void k_events(RenderParams P) {
     Counts cnt{};
     MYRT_STACK(st, lds_stack);
     long long events = 0;
-    (void)pixel_full<false, true, DEEP>(P, i, j, events, st, cnt);
+    (void)pixel_full<false, true, DEEP, WALK>(P, i, j, events, st, cnt);
     P.events[((size_t)slot * 8 + row) * (size_t)P.cam.width + i] = events;
 }
 
@@ -353,8 +364,8 @@ __global__ __launch_bounds__(256) void k_jscan(RenderParams P) {
 }
 
 // Pass 3 (or the only pass without area lights): the render.
-template <bool COUNT, bool DEEP>
-__global__ __launch_bounds__(256) void render_full(RenderParams P) {
+template <bool COUNT, bool DEEP, int WALK>
+__global__ __launch_bounds__(256) MYRT_FULL_ATTR void render_full(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
@@ -365,7 +376,7 @@ __global__ __launch_bounds__(256) void render_full(RenderParams P) {
         MYRT_STACK(st, lds_stack);
         const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;   // packed selection index
         long long jitterIndex = P.num_alights > 0 ? P.jstart[q] : 0;
-        const V3 px = pixel_full<COUNT, false, DEEP>(P, i, j, jitterIndex, st, cnt) / (double)P.cam.samples;
+        const V3 px = pixel_full<COUNT, false, DEEP, WALK>(P, i, j, jitterIndex, st, cnt) / (double)P.cam.samples;
         const size_t o = out_row_of(P, j >> 3, row) * (size_t)P.cam.width + i;
         if (P.out_rgb) {
             P.out_rgb[o * 3 + 0] = px.x;

@@ -105,7 +105,12 @@ def test_grid_vertices_edges_and_faces():
     _check_occluded(sc, O, D, np.full(len(O), 9.999))
 
 
-def test_instances_transforms_and_primitives():
+@pytest.mark.parametrize("walk", ["transformed", "general"])
+def test_instances_transforms_and_primitives(walk, monkeypatch):
+    """Transformed mesh instances, spheres, planes and a triangle: the unified transformed walk
+    (one stack, per-instance ray switches at marker entries, device.h ut_walk) and the nested
+    general walk both give the oracle's intersectTLAS / occludedTLAS bit for bit."""
+    monkeypatch.setenv("MYRT_UT", "1" if walk == "transformed" else "0")
     sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
     base = sc.objects[0]
     sc.objects = [base,
@@ -119,7 +124,9 @@ def test_instances_transforms_and_primitives():
     _check_occluded(sc, O, D, np.random.RandomState(5).uniform(0.1, 6.0, size=len(O)))
 
 
-def test_motion_blur_times_and_tmin():
+@pytest.mark.parametrize("walk", ["transformed", "general"])
+def test_motion_blur_times_and_tmin(walk, monkeypatch):
+    monkeypatch.setenv("MYRT_UT", "1" if walk == "transformed" else "0")
     sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
     base = sc.objects[0]
     base.motion_blur = (0.0, 0.2, 0.0)

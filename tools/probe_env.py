@@ -11,13 +11,13 @@ from myraytracer_amd import scenes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cfg = sys.argv[1]
-sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache")) if cfg == "c3" else \
-    scenes.scene_c5(path_dir=os.path.join(ROOT, "scenes_cache"))
+sc = {"c3": scenes.scene_c3, "c5": scenes.scene_c5, "c3i": scenes.scene_c3_instanced,
+      "c3g": scenes.scene_c3_glass, "c2": scenes.scene_c2}[cfg](path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
 stream = torch.cuda.current_stream()
 out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
-KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE")
+KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE", "MYRT_UT", "MYRT_UNIFIED")
 
 
 def t_frame(k=20):

@@ -12,8 +12,8 @@ if len(sys.argv) > 2 and sys.argv[2] == "--child":
     import myraytracer_amd as M
     from myraytracer_amd import scenes
     cfg = sys.argv[1]
-    sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache")) if cfg == "c3" else \
-        scenes.scene_c5(path_dir=os.path.join(ROOT, "scenes_cache"))
+    sc = {"c3": scenes.scene_c3, "c5": scenes.scene_c5, "c3i": scenes.scene_c3_instanced,
+          "c3g": scenes.scene_c3_glass, "c2": scenes.scene_c2}[cfg](path_dir=os.path.join(ROOT, "scenes_cache"))
     eng = M.RayTracerEngine(sc)
     W, H = sc.cameras[0].image_resolution
     out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
