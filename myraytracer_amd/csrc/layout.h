@@ -132,9 +132,6 @@ struct RenderParams {
     int32_t has_tlas;
     int32_t tlas_leaf_base;          // TriRec count: ~ref >= base means a TLAS leaf
     int32_t identity;                // unified TLAS+BLAS walk allowed (scene.h HostScene::identity)
-    int32_t ut;                      // unified transformed walk allowed (device.h ut_walk; stack bound)
-    int32_t tlas_rec_base;           // records [tlas_rec_base, ...) are TLAS records (ut_walk)
-    int32_t ut_marker_base;          // leaf refs ~e with e >= this are instance markers (ut_walk)
     int32_t num_mats;
     int32_t num_plights;
     DCamera cam;
@@ -181,6 +178,11 @@ struct RenderParams {
                                      // [13] shadow rays traversed, [16..25] per-iteration divergence
                                      // breakdown (rt_work_counters; kCounterWords)
     unsigned long long* wave_times;  // debug (rt_debug_wave_times): per wave {start, end, tile} in 100 MHz ticks
+    // Unified transformed walk (kept at the end, so the fields above keep their kernel-argument
+    // offsets and scalar-load grouping; profiles/r03y_bisect.txt)
+    int32_t ut;                      // unified transformed walk allowed (device.h ut_walk; stack bound)
+    int32_t tlas_rec_base;           // records [tlas_rec_base, ...) are TLAS records (ut_walk)
+    int32_t ut_marker_base;          // leaf refs ~e with e >= this are instance markers (ut_walk)
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

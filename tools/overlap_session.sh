@@ -7,8 +7,8 @@
 set -u
 tag="$1"; cfg="$2"; steps="$3"; warm="${4:-50}"
 case "$cfg" in
-  c5) K="${KERNEL:-render_kernel<false, true, true>}" ;;
-  *)  K="${KERNEL:-render_kernel<false, false, true>}" ;;
+  c5) K="${KERNEL:-render_kernel<false, true, 1, false>}" ;;
+  *)  K="${KERNEL:-render_kernel<false, false, 1, false>}" ;;
 esac
 B="python3 bench.py --config $cfg --steps $steps --warmup $warm --no-cpu-baseline --no-side-paths"
 s=(

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Kernel concurrency of bench.py's pipelined loop, from a rocprofv3 --kernel-trace CSV.
 
-usage: overlap_summary.py --trace DIR --kernel 'render_kernel<false, false, true>'
+usage: overlap_summary.py --trace DIR --kernel 'render_kernel<false, false, 1, false>'
                           --skip W --frames K [--bench gpurun_out/x.json] -o profiles/overlap_c3.json
 
 bench.py validates its Q = 16 framebuffers with one frame each (engine.frame_pipeline),

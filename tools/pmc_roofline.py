@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Roofline summary of the render megakernel from rocprofv3 passes (one counter group per pass).
 
-usage: pmc_roofline.py --kernel 'render_kernel<false, false, true>' --trace DIR --fetch DIR --write DIR
+usage: pmc_roofline.py --kernel 'render_kernel<false, false, 1, false>' --trace DIR --fetch DIR --write DIR
                        --td DIR [--sq DIR] --lib myraytracer_amd/libmyrt.so -o profiles/roofline_c3.json
 
 Per launch (median over the dispatches of that kernel):

@@ -5,7 +5,13 @@
 set -u
 tag="$1"; shift
 B="python3 bench.py --steps 20 --warmup 3 --in-flight 1 --no-cpu-baseline --no-side-paths $*"
-K="${KERNEL:-render_kernel<false, false, true>}"
+# the frame's render kernel: <COUNT, BOUNCE, WALK (1 = identity, 2 = transformed), QUEUE>
+case " $* " in
+  *" --config c5 "*) K="${KERNEL:-render_kernel<false, true, 1, false>}" ;;
+  *" --config c3i "*) K="${KERNEL:-render_kernel<false, false, 2, false>}" ;;
+  *" --config c3g "*) K="${KERNEL:-render_full<false, false, 1>}" ;;
+  *) K="${KERNEL:-render_kernel<false, false, 1, false>}" ;;
+esac
 steps=(
   "${tag}_trace|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_trace -- $B"
   "${tag}_fetch|300|timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_fetch -- $B"
