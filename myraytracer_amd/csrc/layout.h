@@ -93,6 +93,11 @@ constexpr int kJitterCells = 100;    // buildStratifiedJitter 10x10 table (Objec
 
 struct DTlasLeafEntry { int32_t inst; int32_t last; };
 
+// Area-light frames (render_full.h): k_events walks every path once to count the jitterIndex
+// increments; it also logs each closest hit, so render_full shades the same paths without
+// walking them again.  Walk k of pixel q (packed selection index) sits at [k * stride + q].
+struct DHitRec { double t, u, v; int32_t tri, inst; };
+
 // A queued mirror/conductor bounce ray (compacted bounce render, render.hip k_bounce): the
 // child trace(depth + 1) of one sample plus what its parent level adds back,
 // Lo_parent + M_parent * trace(depth + 1) (Object+Extension.swift:189-206, 252-275).
@@ -183,6 +188,9 @@ struct RenderParams {
     int32_t ut;                      // unified transformed walk allowed (device.h ut_walk; stack bound)
     int32_t tlas_rec_base;           // records [tlas_rec_base, ...) are TLAS records (ut_walk)
     int32_t ut_marker_base;          // leaf refs ~e with e >= this are instance markers (ut_walk)
+    int32_t hit_slots;               // logged walks per pixel (DHitRec; 0 = render_full walks them all)
+    DHitRec* hits;
+    int64_t hit_stride;              // pixels of the selection
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

@@ -782,6 +782,8 @@ struct DeviceReplica {
     long long* events = nullptr;              // area-light passes (grown on demand)
     long long* jstart = nullptr;
     int64_t cap_px = 0;
+    DHitRec* hitlog = nullptr;                // k_events' closest-hit log (grown on demand)
+    int64_t hitlog_cap = 0;                   // records
     void* deep = nullptr; int64_t deep_cap = 0;   // deep trace() frames (render_full<.., true>)
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     unsigned long long* wave_times = nullptr; int64_t wave_times_cap = 0;   // rt_debug_wave_times
@@ -838,7 +840,7 @@ static void free_replica(DeviceReplica& r) {
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart); (void)hipFree(r.wave_times);
-    (void)hipFree(r.deep);
+    (void)hipFree(r.deep); (void)hipFree(r.hitlog);
     (void)hipFree(r.arena.base);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
@@ -1144,6 +1146,9 @@ static dim3 render_grid(const RenderParams& P, int threads, int tw = 8) {
     return dim3((unsigned)(((P.cam.width + px - 1) / px) * (8 / (64 / tw)) * P.num_chunks), 1, 1);
 }
 
+// closest hits logged per pixel by k_events for render_full (32 B each): 8 cover the paths of
+// one sample through a few dielectric levels; longer paths walk their remaining rays again
+constexpr int32_t kHitSlots = 8;
 static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count) {
     const int bt = block_threads();
     dim3 block((unsigned)bt, 1, 1);
@@ -1186,6 +1191,19 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
         }
         P.events = r.events;
         P.jstart = r.jstart;
+        // the closest-hit log: render_full reads the first kHitSlots walks of every pixel back
+        // instead of walking them again (MYRT_HITLOG=K overrides, 0 = off; counting launches walk)
+        const int64_t slots = count ? 0 : env_int("MYRT_HITLOG", kHitSlots, 0, 64);
+        if (slots > 0 && slots * px > r.hitlog_cap) {
+            (void)hipFree(r.hitlog);
+            r.hitlog = nullptr; r.hitlog_cap = 0;
+            if (hipMalloc((void**)&r.hitlog, (size_t)(slots * px) * sizeof(DHitRec)) == hipSuccess) r.hitlog_cap = slots * px;
+            else (void)hipGetLastError();             // no log: render_full walks every ray
+        }
+        const bool log = slots > 0 && slots * px <= r.hitlog_cap;
+        P.hits = log ? r.hitlog : nullptr;
+        P.hit_slots = log ? (int32_t)slots : 0;
+        P.hit_stride = px;
         for (int32_t base = 0; base < P.num_chunks; base += batch) {
             P.slot_base = base;
             dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);

@@ -12,9 +12,12 @@
 // row-major order (:288, Renderer.renderChunk).  A lane cannot know how many area-light
 // evaluations the pixels before it made, so area-light frames take three launches:
 //   k_events   - the same paths without lighting, counting evaluations per pixel
-//                (an evaluation = one area light at one hit with computeDirectLight);
+//                (an evaluation = one area light at one hit with computeDirectLight), and
+//                logging each path's closest hits (RenderParams::hits, the first hit_slots
+//                walks of every pixel);
 //   k_jscan    - per-chunk exclusive prefix sum in row-major pixel order;
-//   render_full- the real render, each pixel starting at its prefix.
+//   render_full- the real render, each pixel starting at its prefix; logged hits are read
+//                back instead of walked again (the walk is deterministic: same ray, same hit).
 #pragma once
 
 namespace myrt {
@@ -67,9 +70,17 @@ struct FrameStack {
     }
 };
 
+// This pixel's closest-hit log (k_events writes it, render_full reads it).  k counts the pixel's
+// walks in trace order, which both passes share: the paths do not depend on the lighting.
+struct HitLog {
+    DHitRec* p;           // walk 0 of this pixel
+    size_t stride;
+    int k, cap;
+};
+
 template <bool COUNT, bool EVENTS, bool DEEP, int WALK>
 __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng,
-                         long long& jitterIndex, Stack& st, Counts& c) {
+                         long long& jitterIndex, Stack& st, Counts& c, HitLog& hl) {
     FrameStack<DEEP> F;
     if (DEEP) {
         F.stride = (size_t)gridDim.x * blockDim.x;
@@ -86,7 +97,19 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
             out = LevelOut{v3(0, 0, 0), false, 0, DINF};
         } else {
             Hit h;
-            walk_closest<COUNT, WALK>(P, o, d, rcp(d), tlo, time, h, st, c);
+            const bool logged = hl.k < hl.cap;
+            if (!COUNT && !EVENTS && logged) {
+                const DHitRec r = hl.p[(size_t)hl.k * hl.stride];
+                h.t = r.t; h.u = r.u; h.v = r.v; h.tri = r.tri; h.inst = r.inst;
+            } else {
+                walk_closest<COUNT, WALK>(P, o, d, rcp(d), tlo, time, h, st, c);
+                if (EVENTS && logged) {
+                    DHitRec r;
+                    r.t = h.t; r.u = h.u; r.v = h.v; r.tri = h.tri; r.inst = h.inst;
+                    hl.p[(size_t)hl.k * hl.stride] = r;
+                }
+            }
+            hl.k++;
             if (h.inst < 0) {                                        // :101-103
                 out = LevelOut{ld3(P.background), false, 0, DINF};
             } else {
@@ -265,7 +288,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
 // Pixel loop shared by k_events and render_full (Object+Extension.swift:292-356).
 template <bool COUNT, bool EVENTS, bool DEEP, int WALK>
 __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, long long& jitterIndex, Stack& st,
-                                         Counts& c) {
+                                         Counts& c, HitLog& hl) {
     const DCamera& C = P.cam;
     PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
     V3 pixel = v3(0, 0, 0);
@@ -297,7 +320,7 @@ __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, lo
             const double denom = dot(dir, w);
             const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
             pixel = pixel + trace_full<COUNT, EVENTS, DEEP, WALK>(P, camEye, dir, smax(tImg, 0.0), time, rng, jitterIndex,
-                                                                  st, c);
+                                                                  st, c, hl);
             sampleIndex += 1;
             if (sampleIndex >= C.samples) break;
         }
@@ -335,8 +358,10 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_events(RenderParams P) {
     Counts cnt{};
     MYRT_STACK(st, lds_stack);
     long long events = 0;
-    (void)pixel_full<false, true, DEEP, WALK>(P, i, j, events, st, cnt);
-    P.events[((size_t)slot * 8 + row) * (size_t)P.cam.width + i] = events;
+    const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
+    HitLog hl{P.hits + q, (size_t)P.hit_stride, 0, P.hits ? P.hit_slots : 0};
+    (void)pixel_full<false, true, DEEP, WALK>(P, i, j, events, st, cnt, hl);
+    P.events[q] = events;
 }
 
 // Pass 2: exclusive prefix of the events over each chunk, row-major (one block per chunk).
@@ -376,7 +401,8 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void render_full(RenderParams P
         MYRT_STACK(st, lds_stack);
         const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;   // packed selection index
         long long jitterIndex = P.num_alights > 0 ? P.jstart[q] : 0;
-        const V3 px = pixel_full<COUNT, false, DEEP, WALK>(P, i, j, jitterIndex, st, cnt) / (double)P.cam.samples;
+        HitLog hl{P.hits + q, (size_t)P.hit_stride, 0, P.hits ? P.hit_slots : 0};
+        const V3 px = pixel_full<COUNT, false, DEEP, WALK>(P, i, j, jitterIndex, st, cnt, hl) / (double)P.cam.samples;
         const size_t o = out_row_of(P, j >> 3, row) * (size_t)P.cam.width + i;
         if (P.out_rgb) {
             P.out_rgb[o * 3 + 0] = px.x;

@@ -116,6 +116,22 @@ def test_area_lights_with_dielectric_and_mesh():
     _compare(sc)
 
 
+@pytest.mark.parametrize("slots", ["1", "8", "0"])
+def test_area_light_hit_log(monkeypatch, slots):
+    """render_full reads the closest hits k_events logged instead of walking them again
+    (RenderParams::hits): 8 slots cover most paths here, 1 slot sends every path past its
+    first walk to the fallback walk, 0 turns the log off.  Glass, mirror and a rough
+    dielectric give paths of up to 2^5 - 1 walks; four samples per pixel."""
+    monkeypatch.setenv("MYRT_HITLOG", slots)
+    sc = _area_scene(88, 64, spp=4)
+    sc.objects[1].material = "3"
+    sc.objects[2].material = "2"
+    sc.objects[3].material = "5"
+    sc.max_recursion_depth = 4
+    st = _compare(sc)
+    assert st.secondary_rays > 0
+
+
 def test_c5_10m_mirrors_sampled_chunks_and_full_frame(scene_dir):
     """C5 (BASELINE configs[4]): ~10M triangles in two meshes (TLAS of 2), 3840x2160,
     depth-4 mirror reflections.  SURVEY.md §8d: 'for C5 check a sampled 1/64 of the rows

@@ -17,7 +17,7 @@ eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
 stream = torch.cuda.current_stream()
 out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
-KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE", "MYRT_UT", "MYRT_UNIFIED")
+KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE", "MYRT_UT", "MYRT_UNIFIED", "MYRT_HITLOG")
 
 
 def t_frame(k=20):
