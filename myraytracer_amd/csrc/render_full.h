@@ -87,7 +87,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
         F.deep = reinterpret_cast<Frame*>(P.deep) + ((size_t)blockIdx.x * blockDim.x + threadIdx.x);
     }
     int depth = 0;
-    LevelOut out;
+    LevelOut out{};
     for (;;) {
         // ======================================================== enter level `depth`
         bool descend = false;
@@ -121,7 +121,9 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 const bool frontFacing = dot(d, Ngeo) < 0;
                 const V3 N = frontFacing ? Ngeo : -Ngeo;
                 const bool computeDirect = !(M.ior > 0) || frontFacing;
-                V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+                // EVENTS passes keep only what steers the path (directions, origins, the PCG32
+                // draws, the dielectric's TIR test): no radiance, no Beer data in the frames
+                V3 Lo = (!EVENTS && computeDirect) ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
                 if (computeDirect) {
                     if (!EVENTS) {
                         for (int li = 0; li < P.num_plights; ++li) {        // :118-143
@@ -183,9 +185,11 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                     }
                 }
                 Frame& f = F[depth];
-                f.Lo = Lo; f.p = p; f.t = h.t; f.hitmat = hitmat; f.mat = mi;
+                f.p = p;
+                if (!EVENTS) { f.Lo = Lo; f.t = h.t; f.hitmat = hitmat; f.mat = mi; }
                 if ((M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && depth < P.max_depth) {   // :189-206, :252-275
-                    if (M.type == RT_MAT_MIRROR) {
+                    if (EVENTS) {
+                    } else if (M.type == RT_MAT_MIRROR) {
                         f.aux = ld3(M.mirror);
                     } else {
                         const double cosI = smax(0.0, -dot(d, N));
@@ -228,15 +232,14 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                         const double eta = n1 / n2;
                         f.td = normalize((d * eta) + (mfN * (eta * cosI - cosT)));
                     }
-                    f.R = R;
-                    f.entering = entering;
+                    if (!EVENTS) { f.R = R; f.entering = entering; }
                     f.state = kFrameDielR;
                     c.secondary++;
                     o = p + rd * P.shadow_eps;
                     d = rd;
                     tlo = 0.0;
                     descend = true;
-                } else {
+                } else if (!EVENTS) {
                     out = LevelOut{isfin(Lo) ? Lo : v3(0, 0, 0), true, hitmat, h.t};   // :277-280
                 }
             }
@@ -248,17 +251,19 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
             depth--;
             Frame& f = F[depth];
             if (f.state == kFrameMirror) {
+                if (EVENTS) continue;
                 const V3 Lo = f.Lo + f.aux * out.L;
                 out = LevelOut{isfin(Lo) ? Lo : v3(0, 0, 0), true, f.hitmat, f.t};
                 continue;
             }
             if (f.state == kFrameDielR) {
                 if (f.tir) {
+                    if (EVENTS) continue;
                     const V3 Lo = f.Lo + out.L;
                     out = LevelOut{isfin(Lo) ? Lo : v3(0, 0, 0), true, f.hitmat, f.t};
                     continue;
                 }
-                f.aux = out.L;                                       // LiR
+                if (!EVENTS) f.aux = out.L;                          // LiR
                 f.state = kFrameDielT;
                 c.secondary++;
                 o = f.p + f.td * P.shadow_eps;                       // Ray(origin:dir:time:), tMin 0
@@ -269,6 +274,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 break;
             }
             // kFrameDielT
+            if (EVENTS) continue;
             V3 LiT = out.L;
             const DMaterial& M = P.mats[f.mat];
             const bool absNonZero = !(M.absorption[0] == 0 && M.absorption[1] == 0 && M.absorption[2] == 0);
