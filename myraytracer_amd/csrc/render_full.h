@@ -25,6 +25,11 @@ namespace dev {
 
 enum : int { kFrameMirror = 1, kFrameDielR = 2, kFrameDielT = 3 };
 
+// pow as an out-of-line call: inlined, OCML's pow (extended-precision log, all ranges) adds its
+// working registers to the whole full-trace kernel (cf. device.h phong_pow, which the megakernel
+// uses only where its domain is known)
+__device__ __noinline__ double pow_call(double x, double y) { return pow(x, y); }
+
 struct Frame {            // one suspended trace() level waiting for a child
     V3 Lo;                // radiance of this level so far
     V3 p;                 // hit point (transmission origin)
@@ -124,64 +129,72 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 // EVENTS passes keep only what steers the path (directions, origins, the PCG32
                 // draws, the dielectric's TIR test): no radiance, no Beer data in the frames
                 V3 Lo = (!EVENTS && computeDirect) ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
-                if (computeDirect) {
-                    if (!EVENTS) {
-                        for (int li = 0; li < P.num_plights; ++li) {        // :118-143
+                if (computeDirect && EVENTS) jitterIndex += P.num_alights;   // one per area light (:152-154)
+                if (computeDirect && !EVENTS) {
+                    // point lights (:118-143), then area lights (:145-186), through ONE shadow-walk
+                    // call site (one inlined copy of the walk): each light's contribution is formed
+                    // before its walk - the same expressions on the same values - and added in light
+                    // order when the walk finds the light unblocked
+                    const int nl = P.num_plights + P.num_alights;
+                    for (int li = 0; li < nl; ++li) {
+                        V3 wi, contrib = v3(0, 0, 0);
+                        double tmax = 0.0;
+                        bool trace = false, use = false;
+                        if (li < P.num_plights) {
                             const DPointLight& PL = P.plights[li];
-                            V3 wi = ld3(PL.position) - p;
+                            wi = ld3(PL.position) - p;
                             const double dist = length(wi);
                             wi = normalize(wi);
                             c.shadow++;
                             const double NdotL = smax(0.0, dot(N, wi));
-                            if (NdotL > 0 || MYRT_REF(P)) {                 // else the result is discarded
-                                c.shadow_traced++;
-                                const bool blocked =
-                                    walk_occluded<COUNT, WALK>(P, p + wi * P.shadow_eps, wi, dist, time, st, c);
-                                if (!blocked && NdotL > 0) {
-                                    const double shininess = smax(1.0, M.phong);
-                                    const V3 Ld = ld3(M.diffuse) * NdotL;
-                                    const V3 view = normalize(-d);
-                                    const V3 hv = normalize(wi + view);
-                                    const double NdotH = smax(0.0, dot(N, hv));
-                                    const V3 Ls = ld3(M.specular) * pow(NdotH, shininess);
-                                    const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
-                                    Lo = Lo + (Ld + Ls) * atten;
-                                }
+                            trace = NdotL > 0 || MYRT_REF(P);                  // else the result is discarded
+                            use = NdotL > 0;
+                            tmax = dist;
+                            if (use) {
+                                const double shininess = smax(1.0, M.phong);
+                                const V3 Ld = ld3(M.diffuse) * NdotL;
+                                const V3 view = normalize(-d);
+                                const V3 hv = normalize(wi + view);
+                                const double NdotH = smax(0.0, dot(N, hv));
+                                const V3 Ls = ld3(M.specular) * pow_call(NdotH, shininess);
+                                const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
+                                contrib = (Ld + Ls) * atten;
+                            }
+                        } else {
+                            const DAreaLight& AL = P.alights[li - P.num_plights];
+                            const V3 nL = normalize(ld3(AL.normal));
+                            V3 tg, bt;
+                            onb(nL, tg, bt);
+                            const double size = AL.size;
+                            const double area = size * size;
+                            const int cell = (int)(jitterIndex % kJitterCells);
+                            const double r1 = P.jitter[cell] / 10.0 - 0.5;
+                            const double r2 = P.jitter[kJitterCells + cell] / 10.0 - 0.5;
+                            jitterIndex += 1;
+                            const V3 samplePos = (ld3(AL.position) + tg * (r1 * size)) + bt * (r2 * size);
+                            wi = samplePos - p;
+                            const double dist2 = dot(wi, wi);
+                            const double dist = dsqrt(dist2);
+                            wi = wi / dist;
+                            const double NdotL = dot(N, wi);
+                            const double Ln = fabs(dot(nL, -wi));
+                            if (NdotL > 0 && Ln > 0) {
+                                c.shadow++;
+                                trace = use = true;
+                                tmax = dist - P.shadow_eps;
+                                const V3 view = normalize(-d);
+                                const V3 hv = normalize(wi + view);
+                                const V3 Ld = ld3(M.diffuse) * NdotL;
+                                const V3 Ls = ld3(M.specular) * pow_call(smax(0.0, dot(N, hv)), M.phong);
+                                const V3 brdf = Ld + Ls;
+                                contrib = ((brdf * ld3(AL.radiance)) * (Ln / dist2)) * area;
                             }
                         }
-                    }
-                    for (int ai = 0; ai < P.num_alights; ++ai) {            // :145-186
-                        if (EVENTS) { jitterIndex += 1; continue; }
-                        const DAreaLight& AL = P.alights[ai];
-                        const V3 nL = normalize(ld3(AL.normal));
-                        V3 tg, bt;
-                        onb(nL, tg, bt);
-                        const double size = AL.size;
-                        const double area = size * size;
-                        const int cell = (int)(jitterIndex % kJitterCells);
-                        const double r1 = P.jitter[cell] / 10.0 - 0.5;
-                        const double r2 = P.jitter[kJitterCells + cell] / 10.0 - 0.5;
-                        jitterIndex += 1;
-                        const V3 samplePos = (ld3(AL.position) + tg * (r1 * size)) + bt * (r2 * size);
-                        V3 wi = samplePos - p;
-                        const double dist2 = dot(wi, wi);
-                        const double dist = dsqrt(dist2);
-                        wi = wi / dist;
-                        const double NdotL = dot(N, wi);
-                        if (NdotL <= 0) continue;
-                        const double Ln = fabs(dot(nL, -wi));
-                        if (Ln <= 0) continue;
-                        c.shadow++;
-                        c.shadow_traced++;
-                        if (walk_occluded<COUNT, WALK>(P, p + wi * P.shadow_eps, wi, dist - P.shadow_eps, time, st, c))
-                            continue;
-                        const V3 view = normalize(-d);
-                        const V3 hv = normalize(wi + view);
-                        const V3 Ld = ld3(M.diffuse) * NdotL;
-                        const V3 Ls = ld3(M.specular) * pow(smax(0.0, dot(N, hv)), M.phong);
-                        const V3 brdf = Ld + Ls;
-                        const V3 contrib = ((brdf * ld3(AL.radiance)) * (Ln / dist2)) * area;
-                        Lo = Lo + contrib;
+                        if (trace) {
+                            c.shadow_traced++;
+                            const bool blocked = walk_occluded<COUNT, WALK>(P, p + wi * P.shadow_eps, wi, tmax, time, st, c);
+                            if (!blocked && use) Lo = Lo + contrib;
+                        }
                     }
                 }
                 Frame& f = F[depth];
