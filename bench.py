@@ -12,7 +12,8 @@ of the image and the host gather.  The image is what the reference's public
 time spans Renderer.render + the RGBA8 conversion).  The kernels store the RGBA8 rows
 straight into a page-locked host framebuffer (host-mapped, over PCIe).  The reference's
 render is `async`; frames go through rt_render_submit / rt_render_wait with `--in-flight`
-(default 4) renders in flight, frame k into framebuffer k mod Q, so the next frame's tiles
+(default RT_MAX_IN_FLIGHT = 16) renders in flight on 32 hardware queues, frame k into
+framebuffer k mod Q, so the next frame's tiles
 fill the compute units the previous frame's slowest tiles leave idle; value = K frames
 delivered / wall time.  `timing.submit_to_done_ms` is one frame's latency.  Side fields
 time the FP64 [Vec3] framebuffer delivered synchronously (`fp64_path`, rt_render) and the
@@ -34,9 +35,12 @@ roofline (dominant kernel = the render megakernel, average duration from HIP eve
 its stream, taken inside rt_render): `achieved` = measured HBM bytes per launch (PMC
 FETCH_SIZE x2 + WRITE_SIZE, profiles/roofline_<config>.json, same build) / kernel time,
 against the 8 TB/s HBM peak.  The kernel is not HBM-bound (its working set sits in L2 and
-the 256 MB Infinity Cache): `roofline.binding` names the resource that binds it (the
-vector-memory data path, TD busy from the same profile) and `roofline.reference_work` the
-SURVEY §8(d) algorithmic bytes of the reference's unpruned walk, counted on the GPU.
+the 256 MB Infinity Cache): `roofline.binding` names the resource that binds it (FP64 VALU
+issue at ~half lane utilisation, then the vector-memory data path; from the same profile),
+`roofline.pipelined` divides the same bytes by the GPU time a pipelined frame costs (the union
+of the render launches in the bench's own loop under rocprofv3, profiles/overlap_<config>.json)
+and `roofline.reference_work` holds the SURVEY §8(d) algorithmic bytes of the reference's
+unpruned walk, counted on the GPU.
 cpu_baseline: the C++ restatement of the reference CPU renderer (oracle/, test
 infrastructure), rank 0, N = 1: median over whole frames at the box's CPU share, plus the
 1-thread rate on a sampled subset of chunks.
@@ -486,11 +490,10 @@ def side_paths(eng, first, step, rows, W, H, rays_rank, args):
     return res
 
 
-def cgroup_cpu_quota():
+def cgroup_cpu_quota(path="/sys/fs/cgroup/cpu.max"):
     """CPUs the process may actually use: the cgroup v2 CPU quota (cpu.max = "quota period",
     or "max") - on the GPU box 1600000/100000 = 16 CPUs while the affinity mask shows all 256
-    cores of the machine (profiles/r03a_cpu_probe.txt)."""
-    path = "/sys/fs/cgroup/cpu.max"
+    cores of the machine (profiles/r03a_cpu_probe.txt).  Returns (cpus or None, path, raw)."""
     try:
         with open(path) as fh:
             raw = fh.read().strip()

@@ -1,0 +1,109 @@
+"""The measurement tooling behind bench.py's line (CPU only): the CPU-baseline core count read
+from the cgroup quota, the kernel-overlap summary of a rocprofv3 kernel trace
+(tools/overlap_summary.py, roofline.pipelined) and the PMC roofline summary
+(tools/pmc_roofline.py: FETCH_SIZE x2 on gfx950, VALU busy / lane utilisation)."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import bench  # noqa: E402
+import overlap_summary  # noqa: E402
+
+
+@pytest.mark.parametrize("raw, cpus", [("1600000 100000", 16), ("150000 100000", 2), ("50000 100000", 1),
+                                       ("max 100000", None)])
+def test_cgroup_quota(tmp_path, raw, cpus):
+    f = tmp_path / "cpu.max"
+    f.write_text(raw + "\n")
+    got, path, seen = bench.cgroup_cpu_quota(str(f))
+    assert got == cpus and path == str(f) and seen == raw
+
+
+def test_cgroup_quota_missing(tmp_path):
+    assert bench.cgroup_cpu_quota(str(tmp_path / "absent"))[0] is None
+
+
+def _trace_rows(spans, kernel="render_kernel<false, false, 1, false>"):
+    rows = []
+    for k, (s, e, name) in enumerate(spans):
+        rows.append({"Kernel_Name": f"void myrt::dev::{name or kernel}(myrt::RenderParams)",
+                     "Dispatch_Id": str(k + 1), "Start_Timestamp": str(s), "End_Timestamp": str(e)})
+    return rows
+
+
+def test_overlap_summary_union_and_concurrency():
+    K = "render_kernel<false, false, 1, false>"
+    spans = [(0, 1_000_000, None),                      # a validation frame: skipped
+             (2_000_000, 12_000_000, None),             # timed frame 1
+             (7_000_000, 17_000_000, None),             # timed frame 2, overlaps frame 1 by 5 ms
+             (3_000_000, 4_000_000, "k_counters_out"),  # another kernel inside the window
+             (20_000_000, 30_000_000, None),            # timed frame 3, after a 3 ms gap
+             (40_000_000, 41_000_000, None)]            # a single frame after the timed ones
+    res = overlap_summary.summarize(_trace_rows(spans), K, skip=1, frames=3)
+    # union [2, 17) + [20, 30) = 25 ms over 3 frames; launches sum to 30 ms
+    assert res["union_per_frame_ms"] == pytest.approx(25 / 3, rel=1e-6)
+    assert res["span_per_frame_ms"] == pytest.approx(28 / 3, rel=1e-6)
+    assert res["concurrency"] == pytest.approx(30 / 25, rel=1e-3)
+    assert res["max_overlap"] == 2
+    assert res["time_at_overlap"] == {"1": pytest.approx(20 / 25, abs=1e-4), "2": pytest.approx(5 / 25, abs=1e-4)}
+    assert res["idle_fraction_of_span"] == pytest.approx(3 / 28, abs=1e-5)
+    assert res["other_kernels_in_window"] == {"void myrt::dev::k_counters_out(myrt::RenderParams)":
+                                              {"calls": 1, "total_ms": 1.0}}
+
+
+def test_overlap_summary_needs_enough_dispatches():
+    with pytest.raises(SystemExit):
+        overlap_summary.summarize(_trace_rows([(0, 1, None)]), "render_kernel", skip=1, frames=1)
+
+
+def _write_csv(path, rows):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+
+
+def test_pmc_roofline_summary(tmp_path):
+    K = "render_kernel<false, false, 1, false>"
+    name = f"void myrt::dev::{K}(myrt::RenderParams)"
+    _write_csv(str(tmp_path / "trace/x/1_kernel_stats.csv"),
+               [{"Name": name, "Calls": "45", "AverageNs": "750000.0"},
+                {"Name": "k_counters_out", "Calls": "45", "AverageNs": "4000.0"}])
+
+    def pmc(sub, counters):
+        rows = []
+        for d in (1, 2, 3):                              # three launches; the median is taken
+            for c, v in counters.items():
+                rows.append({"Dispatch_Id": str(d), "Kernel_Name": name, "Counter_Name": c,
+                             "Counter_Value": str(v * (1.0 if d == 2 else (0.5 if d == 1 else 2.0)))})
+        _write_csv(str(tmp_path / sub / "x/1_counter_collection.csv"), rows)
+    pmc("fetch", {"FETCH_SIZE": 87000.0})
+    pmc("write", {"WRITE_SIZE": 11000.0})
+    pmc("td", {"GRBM_GUI_ACTIVE": 15_000_000.0, "TD_TD_BUSY_sum": 340_000_000.0, "TA_BUSY_avr": 700_000.0,
+               "SQ_THREAD_CYCLES_VALU": 10_500_000_000.0})
+    pmc("sq", {"SQ_ACTIVE_INST_VALU": 318_000_000.0})
+    lib = tmp_path / "lib.so"
+    lib.write_bytes(b"not a library")
+    out = tmp_path / "roofline.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_roofline.py"), "--kernel", K,
+                    "--trace", str(tmp_path / "trace"), "--fetch", str(tmp_path / "fetch"),
+                    "--write", str(tmp_path / "write"), "--td", str(tmp_path / "td"), "--sq", str(tmp_path / "sq"),
+                    "--lib", str(lib), "-o", str(out)], check=True, capture_output=True)
+    r = json.loads(out.read_text())
+    assert r["kernel_ms"] == 0.75 and r["trace_calls"] == 45 and r["pmc_launches"] == [3, 3]
+    # gfx950: FETCH_SIZE counts 128-B requests at 64 B -> x2; KB -> bytes
+    assert r["hbm_bytes_per_launch"] == int(87000 * 1024 * 2 + 11000 * 1024)
+    assert r["hbm_GBs"] == pytest.approx((87000 * 2048 + 11000 * 1024) / 0.75e-3 / 1e9, abs=0.1)
+    assert r["td_busy"] == pytest.approx((340e6 / 256) / (15e6 / 8), abs=1e-4)
+    assert r["valu_busy"] == pytest.approx(318e6 / 256 / (15e6 / 8), abs=1e-4)
+    assert r["valu_lane_util"] == pytest.approx(10.5e9 / (64 * 318e6), abs=1e-4)
+    assert len(r["lib_sha256_16"]) == 16
