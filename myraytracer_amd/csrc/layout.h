@@ -97,6 +97,9 @@ struct DTlasLeafEntry { int32_t inst; int32_t last; };
 // increments; it also logs each closest hit, so render_full shades the same paths without
 // walking them again.  Walk k of pixel q (packed selection index) sits at [k * stride + q].
 struct DHitRec { double t, u, v; int32_t tri, inst; };
+// A logged walk's ray, for the node-parallel shading pass (render_full.h k_shade): its origin,
+// direction and time, and the pixel's jitterIndex when the node is shaded (from the pixel's start).
+struct DNodeRec { double o[3], d[3], time; int32_t jofs, hit; };
 
 // A queued mirror/conductor bounce ray (compacted bounce render, render.hip k_bounce): the
 // child trace(depth + 1) of one sample plus what its parent level adds back,
@@ -191,6 +194,13 @@ struct RenderParams {
     int32_t hit_slots;               // logged walks per pixel (DHitRec; 0 = render_full walks them all)
     DHitRec* hits;
     int64_t hit_stride;              // pixels of the selection
+    // node-parallel shading of the logged walks (render_full.h k_shade): k_events records each
+    // logged walk's ray (nodes) and each pixel's walk count (walks); k_shade writes the direct
+    // light of every logged hit (node_lo, 3 doubles, [k * hit_stride + q]); render_full reads it.
+    // nullptr = render_full shades every hit itself.
+    DNodeRec* nodes;
+    double* node_lo;
+    int32_t* walks;
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

@@ -784,6 +784,10 @@ struct DeviceReplica {
     int64_t cap_px = 0;
     DHitRec* hitlog = nullptr;                // k_events' closest-hit log (grown on demand)
     int64_t hitlog_cap = 0;                   // records
+    DNodeRec* nodes = nullptr;                // node-parallel shading: logged rays + direct light
+    double* node_lo = nullptr;
+    int32_t* walks = nullptr;
+    int64_t nodes_cap = 0;                    // records (nodes, node_lo); walks: cap_px
     void* deep = nullptr; int64_t deep_cap = 0;   // deep trace() frames (render_full<.., true>)
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     unsigned long long* wave_times = nullptr; int64_t wave_times_cap = 0;   // rt_debug_wave_times
@@ -841,6 +845,7 @@ static void free_replica(DeviceReplica& r) {
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart); (void)hipFree(r.wave_times);
     (void)hipFree(r.deep); (void)hipFree(r.hitlog);
+    (void)hipFree(r.nodes); (void)hipFree(r.node_lo); (void)hipFree(r.walks);
     (void)hipFree(r.arena.base);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
@@ -1146,10 +1151,19 @@ static dim3 render_grid(const RenderParams& P, int threads, int tw = 8) {
     return dim3((unsigned)(((P.cam.width + px - 1) / px) * (8 / (64 / tw)) * P.num_chunks), 1, 1);
 }
 
-// closest hits logged per pixel by k_events for render_full (32 B each): 8 cover the paths of
-// one sample through a few dielectric levels; longer paths walk their remaining rays again
-constexpr int32_t kHitSlots = 8;
-static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count) {
+// Walks logged per pixel by k_events (hit + ray + direct light: 120 B each): every walk of a
+// pixel's paths when they fit - n*n traced samples, each a trace() tree of at most 2^(D+1) - 1
+// walks with dielectrics (reflection + transmission per level) or D + 1 without - capped at 64 and
+// at kHitLogBytes; walks past the log are walked and shaded by render_full itself.
+constexpr int64_t kHitLogBytes = 16ll << 30;
+static int64_t hit_slots_for(const RenderParams& P, bool dielectric, int64_t px) {
+    const int64_t d = std::min<int64_t>(std::max(0, P.max_depth), 6);
+    const int64_t per_sample = dielectric ? ((int64_t(2) << d) - 1) : d + 1;
+    const int64_t traced = std::max(1, std::min(P.cam.samples, P.cam.n * P.cam.n));
+    const int64_t by_mem = kHitLogBytes / std::max<int64_t>(1, px * (int64_t)(sizeof(DHitRec) + sizeof(DNodeRec) + 24));
+    return std::max<int64_t>(0, std::min<int64_t>({per_sample * traced, 64, by_mem}));
+}
+static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count, bool dielectric) {
     const int bt = block_threads();
     dim3 block((unsigned)bt, 1, 1);
     const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long);
@@ -1191,9 +1205,10 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
         }
         P.events = r.events;
         P.jstart = r.jstart;
-        // the closest-hit log: render_full reads the first kHitSlots walks of every pixel back
+        // the closest-hit log: render_full reads the first `slots` walks of every pixel back
         // instead of walking them again (MYRT_HITLOG=K overrides, 0 = off; counting launches walk)
-        const int64_t slots = count ? 0 : env_int("MYRT_HITLOG", kHitSlots, 0, 64);
+        const int64_t slots =
+            count ? 0 : env_int("MYRT_HITLOG", (int32_t)hit_slots_for(P, dielectric, px), 0, 64);
         if (slots > 0 && slots * px > r.hitlog_cap) {
             (void)hipFree(r.hitlog);
             r.hitlog = nullptr; r.hitlog_cap = 0;
@@ -1204,6 +1219,23 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
         P.hits = log ? r.hitlog : nullptr;
         P.hit_slots = log ? (int32_t)slots : 0;
         P.hit_stride = px;
+        // node-parallel shading of the logged hits (render_full.h k_shade; MYRT_NODESHADE=0: render_full
+        // shades them).  Every pointer a pass writes through is set here, before the first launch:
+        // kernels take RenderParams by value.
+        bool nodeshade = log && env_int("MYRT_NODESHADE", 1, 0, 1) == 1;
+        if (nodeshade && slots * px > r.nodes_cap) {
+            (void)hipFree(r.nodes); (void)hipFree(r.node_lo); (void)hipFree(r.walks);
+            r.nodes = nullptr; r.node_lo = nullptr; r.walks = nullptr; r.nodes_cap = 0;
+            if (hipMalloc((void**)&r.nodes, (size_t)(slots * px) * sizeof(DNodeRec)) == hipSuccess &&
+                hipMalloc((void**)&r.node_lo, (size_t)(slots * px) * 3 * sizeof(double)) == hipSuccess &&
+                hipMalloc((void**)&r.walks, (size_t)px * sizeof(int32_t)) == hipSuccess)
+                r.nodes_cap = slots * px;
+            else (void)hipGetLastError();             // render_full shades every hit
+        }
+        nodeshade = nodeshade && slots * px <= r.nodes_cap;
+        P.nodes = nodeshade ? r.nodes : nullptr;
+        P.node_lo = nodeshade ? r.node_lo : nullptr;
+        P.walks = nodeshade ? r.walks : nullptr;
         for (int32_t base = 0; base < P.num_chunks; base += batch) {
             P.slot_base = base;
             dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);
@@ -1215,6 +1247,13 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
 #undef MYRT_EV0
         }
         hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), dim3(256, 1, 1), 0, stream, P);
+        if (nodeshade) {
+            P.slot_base = 0;                                   // one launch over every chunk
+            const dim3 sgrid(per_slot * (unsigned)P.num_chunks, (unsigned)slots, 1);
+#define MYRT_SH(W_) hipLaunchKernelGGL((dev::k_shade<W_>), sgrid, block, lds, stream, P)
+            MYRT_BY_WALK(MYRT_SH);
+#undef MYRT_SH
+        }
     }
     for (int32_t base = 0; base < P.num_chunks; base += batch) {
         P.slot_base = base;
@@ -1289,7 +1328,7 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     // dielectrics, area lights and maxRecursionDepth > kMaxDepthGPU: the full trace()
     // (render_full.h); it and spheres/planes exist only as megakernels
     const bool full = s->host.has_dielectric || P.num_alights > 0 || P.max_depth > kMaxDepthGPU;
-    if (full) return launch_full(r, P, stream, count);
+    if (full) return launch_full(r, P, stream, count, s->host.has_dielectric);
     if (!use_megakernel() && !P.count_ref && !P.has_special) {   // ref-order counting is a megakernel mode
         const bool bounce_w = scene_has_bounce(s->host) && P.max_depth > 0;
         const int32_t rc = wave_render(P, r.wave, bounce_w, count, stream);

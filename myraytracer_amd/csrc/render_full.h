@@ -75,6 +75,78 @@ struct FrameStack {
     }
 };
 
+// Direct light at a hit (Object+Extension.swift:116-186): point lights (:118-143), then area
+// lights (:145-186), through ONE shadow-walk call site (one inlined copy of the walk): each light's
+// contribution is formed before its walk - the same expressions on the same values - and added to
+// Lo in light order when the walk finds the light unblocked.  jitterIndex advances once per area
+// light (:152-154).
+template <bool COUNT, int WALK>
+__device__ __forceinline__ void direct_light(const RenderParams& P, const DMaterial& M, const V3& N, const V3& p,
+                                             const V3& d, double time, long long& jitterIndex, Stack& st, Counts& c,
+                                             V3& Lo) {
+    const int nl = P.num_plights + P.num_alights;
+    for (int li = 0; li < nl; ++li) {
+        V3 wi, contrib = v3(0, 0, 0);
+        double tmax = 0.0;
+        bool trace = false, use = false;
+        if (li < P.num_plights) {
+            const DPointLight& PL = P.plights[li];
+            wi = ld3(PL.position) - p;
+            const double dist = length(wi);
+            wi = normalize(wi);
+            c.shadow++;
+            const double NdotL = smax(0.0, dot(N, wi));
+            trace = NdotL > 0 || MYRT_REF(P);                  // else the result is discarded
+            use = NdotL > 0;
+            tmax = dist;
+            if (use) {
+                const double shininess = smax(1.0, M.phong);
+                const V3 Ld = ld3(M.diffuse) * NdotL;
+                const V3 view = normalize(-d);
+                const V3 hv = normalize(wi + view);
+                const double NdotH = smax(0.0, dot(N, hv));
+                const V3 Ls = ld3(M.specular) * pow_call(NdotH, shininess);
+                const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
+                contrib = (Ld + Ls) * atten;
+            }
+        } else {
+            const DAreaLight& AL = P.alights[li - P.num_plights];
+            const V3 nL = normalize(ld3(AL.normal));
+            V3 tg, bt;
+            onb(nL, tg, bt);
+            const double size = AL.size;
+            const double area = size * size;
+            const int cell = (int)(jitterIndex % kJitterCells);
+            const double r1 = P.jitter[cell] / 10.0 - 0.5;
+            const double r2 = P.jitter[kJitterCells + cell] / 10.0 - 0.5;
+            jitterIndex += 1;
+            const V3 samplePos = (ld3(AL.position) + tg * (r1 * size)) + bt * (r2 * size);
+            wi = samplePos - p;
+            const double dist2 = dot(wi, wi);
+            const double dist = dsqrt(dist2);
+            wi = wi / dist;
+            const double NdotL = dot(N, wi);
+            const double Ln = fabs(dot(nL, -wi));
+            if (NdotL > 0 && Ln > 0) {
+                c.shadow++;
+                trace = use = true;
+                tmax = dist - P.shadow_eps;
+                const V3 view = normalize(-d);
+                const V3 hv = normalize(wi + view);
+                const V3 Ld = ld3(M.diffuse) * NdotL;
+                const V3 Ls = ld3(M.specular) * pow_call(smax(0.0, dot(N, hv)), M.phong);
+                const V3 brdf = Ld + Ls;
+                contrib = ((brdf * ld3(AL.radiance)) * (Ln / dist2)) * area;
+            }
+        }
+        if (trace) {
+            c.shadow_traced++;
+            const bool blocked = walk_occluded<COUNT, WALK>(P, p + wi * P.shadow_eps, wi, tmax, time, st, c);
+            if (!blocked && use) Lo = Lo + contrib;
+        }
+    }
+}
+
 // This pixel's closest-hit log (k_events writes it, render_full reads it).  k counts the pixel's
 // walks in trace order, which both passes share: the paths do not depend on the lighting.
 struct HitLog {
@@ -112,6 +184,15 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                     DHitRec r;
                     r.t = h.t; r.u = h.u; r.v = h.v; r.tri = h.tri; r.inst = h.inst;
                     hl.p[(size_t)hl.k * hl.stride] = r;
+                    if (P.nodes) {                                   // the ray, for k_shade
+                        DNodeRec n;
+                        n.o[0] = o.x; n.o[1] = o.y; n.o[2] = o.z;
+                        n.d[0] = d.x; n.d[1] = d.y; n.d[2] = d.z;
+                        n.time = time;
+                        n.jofs = (int32_t)jitterIndex;
+                        n.hit = h.inst >= 0 ? 1 : 0;
+                        P.nodes[(size_t)hl.k * hl.stride + (size_t)(hl.p - P.hits)] = n;
+                    }
                 }
             }
             hl.k++;
@@ -131,70 +212,13 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 V3 Lo = (!EVENTS && computeDirect) ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
                 if (computeDirect && EVENTS) jitterIndex += P.num_alights;   // one per area light (:152-154)
                 if (computeDirect && !EVENTS) {
-                    // point lights (:118-143), then area lights (:145-186), through ONE shadow-walk
-                    // call site (one inlined copy of the walk): each light's contribution is formed
-                    // before its walk - the same expressions on the same values - and added in light
-                    // order when the walk finds the light unblocked
-                    const int nl = P.num_plights + P.num_alights;
-                    for (int li = 0; li < nl; ++li) {
-                        V3 wi, contrib = v3(0, 0, 0);
-                        double tmax = 0.0;
-                        bool trace = false, use = false;
-                        if (li < P.num_plights) {
-                            const DPointLight& PL = P.plights[li];
-                            wi = ld3(PL.position) - p;
-                            const double dist = length(wi);
-                            wi = normalize(wi);
-                            c.shadow++;
-                            const double NdotL = smax(0.0, dot(N, wi));
-                            trace = NdotL > 0 || MYRT_REF(P);                  // else the result is discarded
-                            use = NdotL > 0;
-                            tmax = dist;
-                            if (use) {
-                                const double shininess = smax(1.0, M.phong);
-                                const V3 Ld = ld3(M.diffuse) * NdotL;
-                                const V3 view = normalize(-d);
-                                const V3 hv = normalize(wi + view);
-                                const double NdotH = smax(0.0, dot(N, hv));
-                                const V3 Ls = ld3(M.specular) * pow_call(NdotH, shininess);
-                                const V3 atten = ld3(PL.intensity) / smax(dist * dist, 1e-12);
-                                contrib = (Ld + Ls) * atten;
-                            }
-                        } else {
-                            const DAreaLight& AL = P.alights[li - P.num_plights];
-                            const V3 nL = normalize(ld3(AL.normal));
-                            V3 tg, bt;
-                            onb(nL, tg, bt);
-                            const double size = AL.size;
-                            const double area = size * size;
-                            const int cell = (int)(jitterIndex % kJitterCells);
-                            const double r1 = P.jitter[cell] / 10.0 - 0.5;
-                            const double r2 = P.jitter[kJitterCells + cell] / 10.0 - 0.5;
-                            jitterIndex += 1;
-                            const V3 samplePos = (ld3(AL.position) + tg * (r1 * size)) + bt * (r2 * size);
-                            wi = samplePos - p;
-                            const double dist2 = dot(wi, wi);
-                            const double dist = dsqrt(dist2);
-                            wi = wi / dist;
-                            const double NdotL = dot(N, wi);
-                            const double Ln = fabs(dot(nL, -wi));
-                            if (NdotL > 0 && Ln > 0) {
-                                c.shadow++;
-                                trace = use = true;
-                                tmax = dist - P.shadow_eps;
-                                const V3 view = normalize(-d);
-                                const V3 hv = normalize(wi + view);
-                                const V3 Ld = ld3(M.diffuse) * NdotL;
-                                const V3 Ls = ld3(M.specular) * pow_call(smax(0.0, dot(N, hv)), M.phong);
-                                const V3 brdf = Ld + Ls;
-                                contrib = ((brdf * ld3(AL.radiance)) * (Ln / dist2)) * area;
-                            }
-                        }
-                        if (trace) {
-                            c.shadow_traced++;
-                            const bool blocked = walk_occluded<COUNT, WALK>(P, p + wi * P.shadow_eps, wi, tmax, time, st, c);
-                            if (!blocked && use) Lo = Lo + contrib;
-                        }
+                    if (logged && P.node_lo) {                       // shaded by k_shade
+                        const double* lo =
+                            P.node_lo + 3 * ((size_t)(hl.k - 1) * hl.stride + (size_t)(hl.p - P.hits));
+                        Lo = v3(lo[0], lo[1], lo[2]);
+                        jitterIndex += P.num_alights;
+                    } else {
+                        direct_light<COUNT, WALK>(P, M, N, p, d, time, jitterIndex, st, c, Lo);
                     }
                 }
                 Frame& f = F[depth];
@@ -381,6 +405,60 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_events(RenderParams P) {
     HitLog hl{P.hits + q, (size_t)P.hit_stride, 0, P.hits ? P.hit_slots : 0};
     (void)pixel_full<false, true, DEEP, WALK>(P, i, j, events, st, cnt, hl);
     P.events[q] = events;
+    if (P.walks) P.walks[q] = hl.k;
+}
+
+// Node-parallel shading (after k_jscan): the direct light of every logged walk k that hit,
+// one lane per (pixel, k) - the same hit_geometry and direct_light as render_full on the same
+// ray and hit, with the jitterIndex the render pass reaches at that node (the pixel's prefix +
+// the node's offset, both counted by k_events).  Grid: (the selection's tiles, hit_slots).
+// render_full then shades no logged hit itself: its waves no longer run the shadow walks of the
+// longest path tree with the other lanes idle.
+template <int WALK>
+__global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_shade(RenderParams P) {
+    extern __shared__ unsigned long long lds_stack[];
+    int i, j, slot, row;
+    full_pixel_of(P, i, j, slot, row);
+    const int k = (int)blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    Counts cnt{};
+    bool valid = (i < P.cam.width) && (j < P.cam.height);
+    size_t q = 0;
+    if (valid) {
+        q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
+        valid = k < P.walks[q];
+    }
+    if (valid) {
+        const size_t at = (size_t)k * (size_t)P.hit_stride + q;
+        const DNodeRec n = P.nodes[at];
+        if (n.hit) {
+            MYRT_STACK(st, lds_stack);
+            const DHitRec r = P.hits[at];
+            Hit h;
+            h.t = r.t; h.u = r.u; h.v = r.v; h.tri = r.tri; h.inst = r.inst;
+            const V3 o = v3(n.o[0], n.o[1], n.o[2]), d = v3(n.d[0], n.d[1], n.d[2]);
+            V3 p, Ngeo;
+            hit_geometry<false>(P, o, d, n.time, h, p, Ngeo, cnt);
+            const int hitmat = P.insts[h.inst].material;
+            const int mi = max(0, min(P.num_mats - 1, hitmat - 1));
+            const DMaterial& M = P.mats[mi];
+            const bool frontFacing = dot(d, Ngeo) < 0;
+            const V3 N = frontFacing ? Ngeo : -Ngeo;
+            const bool computeDirect = !(M.ior > 0) || frontFacing;
+            V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+            if (computeDirect) {
+                long long jitterIndex = P.jstart[q] + n.jofs;
+                direct_light<false, WALK>(P, M, N, p, d, n.time, jitterIndex, st, cnt, Lo);
+            }
+            double* lo = P.node_lo + 3 * at;
+            lo[0] = Lo.x; lo[1] = Lo.y; lo[2] = Lo.z;
+        }
+    }
+    const unsigned long long s0 = wave_sum(cnt.shadow), s2 = wave_sum(cnt.shadow_traced);
+    if (lane == 0) {
+        if (s0) atomicAdd(&P.counters[0], s0);
+        if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
+    }
 }
 
 // Pass 2: exclusive prefix of the events over each chunk, row-major (one block per chunk).

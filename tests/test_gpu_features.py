@@ -116,13 +116,18 @@ def test_area_lights_with_dielectric_and_mesh():
     _compare(sc)
 
 
-@pytest.mark.parametrize("slots", ["1", "8", "0"])
-def test_area_light_hit_log(monkeypatch, slots):
+@pytest.mark.parametrize("slots, nodeshade", [("auto", "1"), ("auto", "0"), ("1", "1"), ("8", "1"), ("0", "1")])
+def test_area_light_hit_log(monkeypatch, slots, nodeshade):
     """render_full reads the closest hits k_events logged instead of walking them again
-    (RenderParams::hits): 8 slots cover most paths here, 1 slot sends every path past its
-    first walk to the fallback walk, 0 turns the log off.  Glass, mirror and a rough
+    (RenderParams::hits), and k_shade shades the logged hits node-parallel (MYRT_NODESHADE=1,
+    default) or render_full does (0): the default log holds every walk of the paths here, 8 or
+    1 slots send longer paths past the log to the fallback walk, 0 turns the log off.  Glass, mirror and a rough
     dielectric give paths of up to 2^5 - 1 walks; four samples per pixel."""
-    monkeypatch.setenv("MYRT_HITLOG", slots)
+    if slots == "auto":                                  # sized to the scene's path trees (here 31 per sample)
+        monkeypatch.delenv("MYRT_HITLOG", raising=False)
+    else:
+        monkeypatch.setenv("MYRT_HITLOG", slots)
+    monkeypatch.setenv("MYRT_NODESHADE", nodeshade)   # logged hits shaded node-parallel (k_shade) or by render_full
     sc = _area_scene(88, 64, spp=4)
     sc.objects[1].material = "3"
     sc.objects[2].material = "2"

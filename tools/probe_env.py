@@ -17,7 +17,8 @@ eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
 stream = torch.cuda.current_stream()
 out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
-KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE", "MYRT_UT", "MYRT_UNIFIED", "MYRT_HITLOG")
+KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE", "MYRT_UT", "MYRT_UNIFIED", "MYRT_HITLOG",
+        "MYRT_NODESHADE")
 
 
 def t_frame(k=20):
