@@ -201,6 +201,11 @@ struct RenderParams {
     DNodeRec* nodes;
     double* node_lo;
     int32_t* walks;
+    // breadth-first events passes (render_full.h k_level): the log indexed by tree node
+    // (1 = chain, 2 = heap; 0 = the k-th walk), nodes per traced sample, per-node flags
+    int32_t hit_tree;
+    int32_t tree_size;
+    uint8_t* nflags;
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

@@ -493,40 +493,76 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 namespace myrt {
 namespace dev {
 // Per level: the tiles with rays at `level` (their mask is non-zero) and the exclusive prefix of
-// their ray counts, in tile order; totals to the counters.  One block (a few microseconds).
-__global__ __launch_bounds__(1024) void k_qscan(RenderParams P, int level) {
-    __shared__ unsigned s_rays[1024], s_tiles[1024];
-    const int t = threadIdx.x, n = P.bounce_tiles;
+// their ray counts, in tile order; totals to the counters.  Two passes over blocks of
+// kQScanTiles tiles (4 consecutive tiles per thread, coalesced): k_qcount writes each block's
+// (rays, tiles) totals, k_qscan prefixes them and writes the list.  (One 1024-thread block
+// walking the whole mask took ~250 us per level on C5.)
+constexpr int kQScanThreads = 256, kQScanTiles = 4 * kQScanThreads;
+__device__ __forceinline__ unsigned long long* qscan_blocks(const RenderParams& P) {
+    return reinterpret_cast<unsigned long long*>(P.bact + 2 * (size_t)P.bounce_tiles);
+}
+// this thread's 4 tiles: per-tile ray counts, packed (rays | tiles << 32) total
+__device__ __forceinline__ unsigned long long qscan_tiles(const RenderParams& P, int level, int base, unsigned c[4]) {
+    const int n = P.bounce_tiles;
     const unsigned long long* m = P.bmask + (size_t)(level - 1) * n;
-    const int per = (n + 1023) / 1024;
-    const int b = min(n, t * per), e = min(n, b + per);
-    unsigned rays = 0, tiles = 0;
-    for (int k = b; k < e; ++k) {
-        const unsigned c = (unsigned)__popcll(m[k]);
-        rays += c;
-        tiles += c ? 1u : 0u;
+    unsigned long long tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        c[k] = base + k < n ? (unsigned)__popcll(m[base + k]) : 0u;
+        tot += (unsigned long long)c[k] | (c[k] ? (1ull << 32) : 0ull);
     }
-    s_rays[t] = rays; s_tiles[t] = tiles;
+    return tot;
+}
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long x, unsigned long long* s_w) {
+    x = wave_sum(x);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = x;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {                        // inclusive scans
-        const unsigned r = t >= off ? s_rays[t - off] : 0u, q = t >= off ? s_tiles[t - off] : 0u;
-        __syncthreads();
-        s_rays[t] += r; s_tiles[t] += q;
-        __syncthreads();
+    unsigned long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kQScanThreads / 64; ++w) t += s_w[w];
+    __syncthreads();
+    return t;
+}
+__global__ __launch_bounds__(kQScanThreads) void k_qcount(RenderParams P, int level) {
+    __shared__ unsigned long long s_w[kQScanThreads / 64];
+    unsigned c[4];
+    const unsigned long long tot =
+        block_sum_u64(qscan_tiles(P, level, blockIdx.x * kQScanTiles + threadIdx.x * 4, c), s_w);
+    if (threadIdx.x == 0) qscan_blocks(P)[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(kQScanThreads) void k_qscan(RenderParams P, int level) {
+    __shared__ unsigned long long s_w[kQScanThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, n = P.bounce_tiles;
+    const unsigned long long* blk = qscan_blocks(P);
+    unsigned long long before = 0;                       // the blocks before this one
+    for (int k = t; k < (int)blockIdx.x; k += kQScanThreads) before += blk[k];
+    before = block_sum_u64(before, s_w);
+    unsigned c[4];
+    const int base = blockIdx.x * kQScanTiles + t * 4;
+    const unsigned long long mine = qscan_tiles(P, level, base, c);
+    unsigned long long inc = mine;                       // inclusive scan over the wave, then the block
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
     }
-    unsigned run = s_rays[t] - rays, at = s_tiles[t] - tiles;
-    for (int k = b; k < e; ++k) {
-        const unsigned c = (unsigned)__popcll(m[k]);
-        if (c) {
-            P.bact[at] = (uint32_t)k;
+    if (lane == 63) s_w[t >> 6] = inc;
+    __syncthreads();
+    unsigned long long ex = before + inc - mine;
+    for (int w = 0; w < (t >> 6); ++w) ex += s_w[w];
+    unsigned run = (unsigned)ex, at = (unsigned)(ex >> 32);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (c[k]) {
+            P.bact[at] = (uint32_t)(base + k);
             P.bact[n + at] = run;
             ++at;
-            run += c;
+            run += c[k];
         }
     }
-    if (t == 1023) {
-        P.counters[kQueueCount + level] = s_rays[1023];
-        P.counters[kQueueTiles + level] = s_tiles[1023];
+    if (blockIdx.x == gridDim.x - 1 && t == kQScanThreads - 1) {
+        P.counters[kQueueCount + level] = run;
+        P.counters[kQueueTiles + level] = at;
     }
 }
 
@@ -750,6 +786,31 @@ constexpr int64_t kQueueBytesCap = 16ll << 30;
 // Off by default: parity-green but slower than the bounce megakernel on C5 (DESIGN.md §4,
 // "Compacted bounce render"); MYRT_QUEUE=1 selects it.
 constexpr int32_t kQueueDefault = 0;
+// rt_render_submit: full trace() renders (render_full.h) overlapping on their own slot streams,
+// each slot with its own pass scratch (C3g: ~7.8 GB per slot); MYRT_FULL_FLIGHTS overrides
+constexpr int32_t kFullFlights = 4;
+// Scratch of the full trace() passes (render_full.h), grown on demand: per-pixel area-light
+// event counts and jitter prefixes, the closest-hit log, the node-parallel shading records and
+// the level passes' node flags.  The replica has one (rt_render, in-order renders) and each
+// of the first kFullFlights in-flight slots one (rt_render_submit: overlapping full renders).
+struct FullScratch {
+    long long* events = nullptr;
+    long long* jstart = nullptr;
+    int64_t cap_px = 0;
+    DHitRec* hitlog = nullptr;                // records
+    int64_t hitlog_cap = 0;
+    DNodeRec* nodes = nullptr;                // node-parallel shading: logged rays + direct light
+    double* node_lo = nullptr;
+    int32_t* walks = nullptr;
+    int64_t nodes_cap = 0, walks_cap = 0;     // records (nodes, node_lo); pixels (walks)
+    uint8_t* nflags = nullptr;                // level passes: per-node flags
+    int64_t nflags_cap = 0;
+    void release() {
+        (void)hipFree(events); (void)hipFree(jstart); (void)hipFree(hitlog);
+        (void)hipFree(nodes); (void)hipFree(node_lo); (void)hipFree(walks); (void)hipFree(nflags);
+        *this = FullScratch{};
+    }
+};
 struct Flight {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
@@ -764,6 +825,7 @@ struct Flight {
     bool counters_valid = false;                   // host_counters hold this render's counts (k_counters_out ran)
     bool used = false;                             // this replica took part in the render
     BounceArena arena;                             // compacted bounce render queues of this slot
+    FullScratch full;                              // full trace() passes of the renders on this slot's stream
 };
 
 struct DeviceReplica {
@@ -779,15 +841,7 @@ struct DeviceReplica {
     DPointLight* plights = nullptr;
     DAreaLight* alights = nullptr;
     double* jitter = nullptr;
-    long long* events = nullptr;              // area-light passes (grown on demand)
-    long long* jstart = nullptr;
-    int64_t cap_px = 0;
-    DHitRec* hitlog = nullptr;                // k_events' closest-hit log (grown on demand)
-    int64_t hitlog_cap = 0;                   // records
-    DNodeRec* nodes = nullptr;                // node-parallel shading: logged rays + direct light
-    double* node_lo = nullptr;
-    int32_t* walks = nullptr;
-    int64_t nodes_cap = 0;                    // records (nodes, node_lo); walks: cap_px
+    FullScratch full;                         // full trace() passes on the replica stream
     void* deep = nullptr; int64_t deep_cap = 0;   // deep trace() frames (render_full<.., true>)
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     unsigned long long* wave_times = nullptr; int64_t wave_times_cap = 0;   // rt_debug_wave_times
@@ -843,9 +897,9 @@ static void free_replica(DeviceReplica& r) {
     wave_release(r.wave);
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
-    (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.events); (void)hipFree(r.jstart); (void)hipFree(r.wave_times);
-    (void)hipFree(r.deep); (void)hipFree(r.hitlog);
-    (void)hipFree(r.nodes); (void)hipFree(r.node_lo); (void)hipFree(r.walks);
+    (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.wave_times);
+    (void)hipFree(r.deep);
+    r.full.release();
     (void)hipFree(r.arena.base);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
@@ -858,6 +912,7 @@ static void free_replica(DeviceReplica& r) {
         if (f.done) (void)hipEventDestroy(f.done);
         if (f.stream) (void)hipStreamDestroy(f.stream);
         (void)hipFree(f.counters);
+        f.full.release();
         (void)hipFree(f.stage_rgb);
         (void)hipFree(f.stage_rgba);
         (void)hipFree(f.arena.base);
@@ -1124,6 +1179,17 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     return P;
 }
 
+// a material some instance shades with (hits take the instance's material, clamped) is rough
+static bool scene_is_rough(const HostScene& S) {
+    if (S.mats.empty()) return false;
+    for (const auto& I : S.insts) {
+        const int mi = std::max(0, std::min((int)S.mats.size() - 1, (int)I.material - 1));
+        if (S.mats[mi].roughness != 0.0) return true;
+    }
+    return false;
+}
+// breadth-first events passes for area-light frames (render_full.h k_level; MYRT_LEVELS)
+constexpr int32_t kLevelsDefault = 1;
 static bool scene_has_bounce(const HostScene& S) {
     for (const auto& m : S.mats) if (m.type == RT_MAT_MIRROR || m.type == RT_MAT_CONDUCTOR) return true;
     return false;
@@ -1163,7 +1229,8 @@ static int64_t hit_slots_for(const RenderParams& P, bool dielectric, int64_t px)
     const int64_t by_mem = kHitLogBytes / std::max<int64_t>(1, px * (int64_t)(sizeof(DHitRec) + sizeof(DNodeRec) + 24));
     return std::max<int64_t>(0, std::min<int64_t>({per_sample * traced, 64, by_mem}));
 }
-static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream, bool count, bool dielectric) {
+static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hipStream_t stream, bool count, bool dielectric,
+                           bool rough) {
     const int bt = block_threads();
     dim3 block((unsigned)bt, 1, 1);
     const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long);
@@ -1195,48 +1262,83 @@ static int32_t launch_full(DeviceReplica& r, RenderParams P, hipStream_t stream,
     } while (0)
     if (P.num_alights > 0) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
-        if (px > r.cap_px) {
-            (void)hipFree(r.events); (void)hipFree(r.jstart);
-            r.events = nullptr; r.jstart = nullptr; r.cap_px = 0;
-            if (hipMalloc((void**)&r.events, px * sizeof(long long)) != hipSuccess ||
-                hipMalloc((void**)&r.jstart, px * sizeof(long long)) != hipSuccess)
+        if (px > fs.cap_px) {
+            (void)hipFree(fs.events); (void)hipFree(fs.jstart);
+            fs.events = nullptr; fs.jstart = nullptr; fs.cap_px = 0;
+            if (hipMalloc((void**)&fs.events, px * sizeof(long long)) != hipSuccess ||
+                hipMalloc((void**)&fs.jstart, px * sizeof(long long)) != hipSuccess)
                 return fail(RT_ERR_OOM, "device allocation of area-light jitter buffers failed");
-            r.cap_px = px;
+            fs.cap_px = px;
         }
-        P.events = r.events;
-        P.jstart = r.jstart;
+        P.events = fs.events;
+        P.jstart = fs.jstart;
         // the closest-hit log: render_full reads the first `slots` walks of every pixel back
         // instead of walking them again (MYRT_HITLOG=K overrides, 0 = off; counting launches walk)
         const int64_t slots =
             count ? 0 : env_int("MYRT_HITLOG", (int32_t)hit_slots_for(P, dielectric, px), 0, 64);
-        if (slots > 0 && slots * px > r.hitlog_cap) {
-            (void)hipFree(r.hitlog);
-            r.hitlog = nullptr; r.hitlog_cap = 0;
-            if (hipMalloc((void**)&r.hitlog, (size_t)(slots * px) * sizeof(DHitRec)) == hipSuccess) r.hitlog_cap = slots * px;
+        if (slots > 0 && slots * px > fs.hitlog_cap) {
+            (void)hipFree(fs.hitlog);
+            fs.hitlog = nullptr; fs.hitlog_cap = 0;
+            if (hipMalloc((void**)&fs.hitlog, (size_t)(slots * px) * sizeof(DHitRec)) == hipSuccess) fs.hitlog_cap = slots * px;
             else (void)hipGetLastError();             // no log: render_full walks every ray
         }
-        const bool log = slots > 0 && slots * px <= r.hitlog_cap;
-        P.hits = log ? r.hitlog : nullptr;
+        const bool log = slots > 0 && slots * px <= fs.hitlog_cap;
+        P.hits = log ? fs.hitlog : nullptr;
         P.hit_slots = log ? (int32_t)slots : 0;
         P.hit_stride = px;
         // node-parallel shading of the logged hits (render_full.h k_shade; MYRT_NODESHADE=0: render_full
         // shades them).  Every pointer a pass writes through is set here, before the first launch:
         // kernels take RenderParams by value.
         bool nodeshade = log && env_int("MYRT_NODESHADE", 1, 0, 1) == 1;
-        if (nodeshade && slots * px > r.nodes_cap) {
-            (void)hipFree(r.nodes); (void)hipFree(r.node_lo); (void)hipFree(r.walks);
-            r.nodes = nullptr; r.node_lo = nullptr; r.walks = nullptr; r.nodes_cap = 0;
-            if (hipMalloc((void**)&r.nodes, (size_t)(slots * px) * sizeof(DNodeRec)) == hipSuccess &&
-                hipMalloc((void**)&r.node_lo, (size_t)(slots * px) * 3 * sizeof(double)) == hipSuccess &&
-                hipMalloc((void**)&r.walks, (size_t)px * sizeof(int32_t)) == hipSuccess)
-                r.nodes_cap = slots * px;
-            else (void)hipGetLastError();             // render_full shades every hit
+        if (nodeshade && (slots * px > fs.nodes_cap || px > fs.walks_cap)) {
+            const int64_t recs = std::max(slots * px, fs.nodes_cap), pxs = std::max(px, fs.walks_cap);
+            (void)hipFree(fs.nodes); (void)hipFree(fs.node_lo); (void)hipFree(fs.walks);
+            fs.nodes = nullptr; fs.node_lo = nullptr; fs.walks = nullptr; fs.nodes_cap = fs.walks_cap = 0;
+            if (hipMalloc((void**)&fs.nodes, (size_t)recs * sizeof(DNodeRec)) == hipSuccess &&
+                hipMalloc((void**)&fs.node_lo, (size_t)recs * 3 * sizeof(double)) == hipSuccess &&
+                hipMalloc((void**)&fs.walks, (size_t)pxs * sizeof(int32_t)) == hipSuccess) {
+                fs.nodes_cap = recs;
+                fs.walks_cap = pxs;
+            } else {
+                (void)hipGetLastError();              // render_full shades every hit
+            }
         }
-        nodeshade = nodeshade && slots * px <= r.nodes_cap;
-        P.nodes = nodeshade ? r.nodes : nullptr;
-        P.node_lo = nodeshade ? r.node_lo : nullptr;
-        P.walks = nodeshade ? r.walks : nullptr;
-        for (int32_t base = 0; base < P.num_chunks; base += batch) {
+        nodeshade = nodeshade && slots * px <= fs.nodes_cap && px <= fs.walks_cap;
+        P.nodes = nodeshade ? fs.nodes : nullptr;
+        P.node_lo = nodeshade ? fs.node_lo : nullptr;
+        P.walks = nodeshade ? fs.walks : nullptr;
+        // Breadth-first events passes (render_full.h k_level) when the log holds every pixel's
+        // whole trace() trees and no material is rough (no PCG32 draw inside trace(), so the
+        // order of the walks is free); MYRT_LEVELS=0 keeps the depth-first k_events.
+        const int32_t tree = dielectric ? 2 : 1;
+        const int64_t traced = std::max(1, std::min(P.cam.samples, P.cam.n * P.cam.n));
+        const int64_t tree_size = P.max_depth >= 0 && P.max_depth <= 5
+                                      ? (tree == 2 ? (int64_t(2) << P.max_depth) - 1 : P.max_depth + 1) : 0;
+        bool levels = nodeshade && !deep && P.has_tlas && tree_size > 0 && slots == tree_size * traced &&
+                      !rough && env_int("MYRT_LEVELS", kLevelsDefault, 0, 1) == 1;
+        if (levels && slots * px > fs.nflags_cap) {
+            (void)hipFree(fs.nflags);
+            fs.nflags = nullptr; fs.nflags_cap = 0;
+            if (hipMalloc((void**)&fs.nflags, (size_t)(slots * px)) == hipSuccess) fs.nflags_cap = slots * px;
+            else (void)hipGetLastError();             // depth-first k_events
+        }
+        levels = levels && slots * px <= fs.nflags_cap;
+        P.hit_tree = levels ? tree : 0;
+        P.tree_size = levels ? (int32_t)tree_size : 0;
+        P.nflags = levels ? fs.nflags : nullptr;
+        if (levels) {
+            HIP_TRY(hipMemsetAsync(fs.nflags, 0, (size_t)(slots * px), stream));
+            P.slot_base = 0;
+            const unsigned g0 = per_slot * (unsigned)P.num_chunks;
+#define MYRT_LV(W_) hipLaunchKernelGGL((dev::k_level<W_>), dim3(g0, ly, 1), block, lds, stream, P, level)
+            for (int32_t level = 0; level <= P.max_depth; ++level) {
+                const unsigned ly = level == 0 ? 1u : (unsigned)traced * (tree == 2 ? (1u << level) : 1u);
+                MYRT_BY_WALK(MYRT_LV);
+            }
+#undef MYRT_LV
+            hipLaunchKernelGGL(dev::k_jofs, dim3(g0), block, 0, stream, P);
+        }
+        for (int32_t base = 0; base < P.num_chunks && !levels; base += batch) {
             P.slot_base = base;
             dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);
 #define MYRT_EV1(W_) hipLaunchKernelGGL((dev::k_events<true, W_>), grid, block, lds, stream, P)
@@ -1293,7 +1395,8 @@ static bool queue_arena(BounceArena* arena, RenderParams& P, int64_t tiles) {
     // previous launch (whatever its size) zeroed them
     auto bytes = [](int64_t lv, int64_t tl) {
         return (size_t)(lv * tl * 64) * sizeof(BounceRec) + (size_t)(lv * tl) * sizeof(unsigned long long) +
-               (size_t)(2 * tl) * sizeof(uint32_t);
+               (size_t)(2 * tl) * sizeof(uint32_t) +
+               (size_t)((tl + dev::kQScanTiles - 1) / dev::kQScanTiles) * sizeof(unsigned long long);
     };
     if (levels > arena->levels || tiles > arena->tiles) {
         const int64_t lv = std::max(levels, arena->levels), tl = std::max(tiles, arena->tiles);
@@ -1322,13 +1425,14 @@ static bool queue_arena(BounceArena* arena, RenderParams& P, int64_t tiles) {
 }
 
 static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P0, hipStream_t stream, bool count,
-                      BounceArena* arena = nullptr) {
+                      BounceArena* arena = nullptr, FullScratch* full_scratch = nullptr) {
     RenderParams P = P0;
     if (P.num_chunks == 0) return RT_OK;
     // dielectrics, area lights and maxRecursionDepth > kMaxDepthGPU: the full trace()
     // (render_full.h); it and spheres/planes exist only as megakernels
     const bool full = s->host.has_dielectric || P.num_alights > 0 || P.max_depth > kMaxDepthGPU;
-    if (full) return launch_full(r, P, stream, count, s->host.has_dielectric);
+    if (full) return launch_full(r, full_scratch ? *full_scratch : r.full, P, stream, count, s->host.has_dielectric,
+                                 scene_is_rough(s->host));
     if (!use_megakernel() && !P.count_ref && !P.has_special) {   // ref-order counting is a megakernel mode
         const bool bounce_w = scene_has_bounce(s->host) && P.max_depth > 0;
         const int32_t rc = wave_render(P, r.wave, bounce_w, count, stream);
@@ -1363,8 +1467,12 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
 #undef MYRT_QPRIM
         const dim3 qgrid((unsigned)(r.cus * 4 * MYRT_QUEUE_WPE)), qblock(64);
         const size_t qlds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
-        for (int32_t level = 1; level <= P.max_depth; ++level) {
-            hipLaunchKernelGGL(dev::k_qscan, dim3(1), dim3(1024), 0, stream, P, level);
+        const dim3 sgrid((unsigned)((P.bounce_tiles + dev::kQScanTiles - 1) / dev::kQScanTiles));
+        // MYRT_QUEUE_LEVELS (timing probe only: frames are incomplete below max_depth)
+        const int32_t levels = env_int("MYRT_QUEUE_LEVELS", P.max_depth, 0, P.max_depth);
+        for (int32_t level = 1; level <= levels; ++level) {
+            hipLaunchKernelGGL(dev::k_qcount, sgrid, dim3(dev::kQScanThreads), 0, stream, P, level);
+            hipLaunchKernelGGL(dev::k_qscan, sgrid, dim3(dev::kQScanThreads), 0, stream, P, level);
 #define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), qgrid, qblock, qlds, stream, P, level)
             MYRT_BY_WALK(MYRT_QB);
 #undef MYRT_QB
@@ -1615,10 +1723,15 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
     if (fp.pending)
         return fail(RT_ERR_BUSY, "too many renders in flight: wait for ticket " + std::to_string(fp.ticket) + " first");
     const int32_t D = (int32_t)s->devs.size();
-    // dielectrics / area lights / deep recursion (render_full) and the wavefront pipeline use
-    // per-replica scratch buffers: those renders stay on the replica's own stream, in order
-    const bool concurrent = !(s->host.has_dielectric || !s->host.alights.empty() || s->host.max_depth > kMaxDepthGPU) &&
-                            use_megakernel();
+    // Full trace() renders (dielectrics, area lights: render_full) take the stream and pass
+    // scratch of slot q % kFullFlights, so up to kFullFlights of them overlap; deep recursion (one
+    // deep-frame buffer per replica) and the wavefront pipeline (per-replica queues) stay on the
+    // replica's own stream, in order.
+    const bool full = s->host.has_dielectric || !s->host.alights.empty() || s->host.max_depth > kMaxDepthGPU;
+    const int32_t full_flights = env_int("MYRT_FULL_FLIGHTS", kFullFlights, 0, kInFlight);
+    const bool full_slots = full && s->host.max_depth <= kMaxDepthGPU && full_flights > 0;
+    const bool concurrent = full ? full_slots : use_megakernel();
+    const int qs = full_slots ? q % full_flights : q;  // the slot whose stream (and full scratch) it takes
     const auto t0 = std::chrono::steady_clock::now();
     // the caller's buffers mapped for every replica BEFORE anything is launched: a replica
     // that cannot map them must not leave the others' kernels writing into them
@@ -1647,7 +1760,7 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         const int32_t myFirst = first + k * step, myStep = step * D;
         HIP_TRY(hipSetDevice(r.device));
         if (k == fail_at) return fail(RT_ERR_DEVICE, "injected launch failure (MYRT_DEBUG_FAIL_REPLICA)");
-        hipStream_t st = concurrent ? f.stream : r.stream;
+        hipStream_t st = concurrent ? r.fl[qs].stream : r.stream;
         int32_t nq = 0;
         for (int32_t c = myFirst; c < num_chunks_total(H); c += myStep) nq++;
         if (dma) {
@@ -1672,7 +1785,8 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
             P.out_first = frame ? 0 : first;
             P.out_step = frame ? 1 : step;
         }                                                // else packed rows of this replica's chunks
-        const int32_t rc = launch(s, r, P, st, false, concurrent ? &f.arena : &r.arena);
+        const int32_t rc = launch(s, r, P, st, false, concurrent ? &f.arena : &r.arena,
+                                  full_slots ? &r.fl[qs].full : nullptr);
         if (rc != RT_OK) return rc;
         if (dma == 1) {
             // chunk q of this replica = selection entry k + q*D = image chunk myFirst + q*myStep;
@@ -1717,7 +1831,7 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
                 Flight& f = s->devs[j].fl[q];
                 if (!f.used) continue;
                 (void)hipSetDevice(s->devs[j].device);
-                (void)hipStreamSynchronize(concurrent ? f.stream : s->devs[j].stream);
+                (void)hipStreamSynchronize(concurrent ? s->devs[j].fl[qs].stream : s->devs[j].stream);
                 f.used = false;
                 f.counters_zero = false;
             }

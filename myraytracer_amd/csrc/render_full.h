@@ -149,11 +149,17 @@ __device__ __forceinline__ void direct_light(const RenderParams& P, const DMater
 
 // This pixel's closest-hit log (k_events writes it, render_full reads it).  k counts the pixel's
 // walks in trace order, which both passes share: the paths do not depend on the lighting.
+// Tree-indexed logs (P.hit_tree != 0, the breadth-first events passes below): node h of traced
+// sample s at entry s * tree_size + h instead of the k-th walk.
 struct HitLog {
     DHitRec* p;           // walk 0 of this pixel
     size_t stride;
     int k, cap;
+    int tree = 0, node = 0, sbase = 0;
 };
+enum : uint8_t { kNodeExists = 1, kNodeEval = 2 };
+__device__ __forceinline__ int tree_child(int b, int h, int which) { return b == 2 ? 2 * h + 1 + which : h + 1; }
+__device__ __forceinline__ int tree_parent(int b, int h) { return b == 2 ? (h - 1) >> 1 : h - 1; }
 
 template <bool COUNT, bool EVENTS, bool DEEP, int WALK>
 __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng,
@@ -174,9 +180,10 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
             out = LevelOut{v3(0, 0, 0), false, 0, DINF};
         } else {
             Hit h;
-            const bool logged = hl.k < hl.cap;
+            const int kk = hl.tree ? hl.sbase + hl.node : hl.k;     // this walk's log entry
+            const bool logged = kk < hl.cap;
             if (!COUNT && !EVENTS && logged) {
-                const DHitRec r = hl.p[(size_t)hl.k * hl.stride];
+                const DHitRec r = hl.p[(size_t)kk * hl.stride];
                 h.t = r.t; h.u = r.u; h.v = r.v; h.tri = r.tri; h.inst = r.inst;
             } else {
                 walk_closest<COUNT, WALK>(P, o, d, rcp(d), tlo, time, h, st, c);
@@ -214,7 +221,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 if (computeDirect && !EVENTS) {
                     if (logged && P.node_lo) {                       // shaded by k_shade
                         const double* lo =
-                            P.node_lo + 3 * ((size_t)(hl.k - 1) * hl.stride + (size_t)(hl.p - P.hits));
+                            P.node_lo + 3 * ((size_t)kk * hl.stride + (size_t)(hl.p - P.hits));
                         Lo = v3(lo[0], lo[1], lo[2]);
                         jitterIndex += P.num_alights;
                     } else {
@@ -242,6 +249,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                         rd = normalize(rd);
                     }
                     f.state = kFrameMirror;
+                    if (hl.tree) hl.node = tree_child(hl.tree, hl.node, 0);
                     c.secondary++;
                     o = p + N * P.shadow_eps;
                     d = rd;
@@ -271,6 +279,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                     }
                     if (!EVENTS) { f.R = R; f.entering = entering; }
                     f.state = kFrameDielR;
+                    if (hl.tree) hl.node = tree_child(hl.tree, hl.node, 0);
                     c.secondary++;
                     o = p + rd * P.shadow_eps;
                     d = rd;
@@ -286,6 +295,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
         for (;;) {
             if (depth == 0) return out.L;
             depth--;
+            if (hl.tree) hl.node = tree_parent(hl.tree, hl.node);
             Frame& f = F[depth];
             if (f.state == kFrameMirror) {
                 if (EVENTS) continue;
@@ -302,6 +312,7 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 }
                 if (!EVENTS) f.aux = out.L;                          // LiR
                 f.state = kFrameDielT;
+                if (hl.tree) hl.node = tree_child(hl.tree, hl.node, 1);
                 c.secondary++;
                 o = f.p + f.td * P.shadow_eps;                       // Ray(origin:dir:time:), tMin 0
                 d = f.td;
@@ -364,6 +375,7 @@ __device__ __forceinline__ V3 pixel_full(const RenderParams& P, int i, int j, lo
             const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
             pixel = pixel + trace_full<COUNT, EVENTS, DEEP, WALK>(P, camEye, dir, smax(tImg, 0.0), time, rng, jitterIndex,
                                                                   st, c, hl);
+            if (hl.tree) { hl.sbase += P.tree_size; hl.node = 0; }
             sampleIndex += 1;
             if (sampleIndex >= C.samples) break;
         }
@@ -408,6 +420,172 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_events(RenderParams P) {
     if (P.walks) P.walks[q] = hl.k;
 }
 
+// ---- breadth-first events passes (P.hit_tree != 0) -------------------------------------------
+// Without rough materials no PCG32 draw happens inside trace() (:193-198, :209-216, :258-263), so
+// a trace() tree's rays do not depend on the order its nodes are walked in.  Then k_events'
+// depth-first walk of every pixel's tree (a wave runs as long as its deepest tree, lane by lane)
+// becomes one pass per tree level: k_level(0) walks every pixel's primary rays (coherent), and
+// k_level(L) the level-L nodes, one grid row per node position, so a wave holds the same node of
+// 64 neighbouring pixels.  Node h of sample s sits at log entry s * tree_size + h: heap order with
+// dielectrics (reflection child 2h + 1, transmission 2h + 2; hit_tree = 2), the chain h = depth
+// without (hit_tree = 1); the log holds the whole tree.  A parent writes its children's rays
+// (DNodeRec o, d, time) and existence flags; k_jofs then visits each pixel's nodes in trace()'s
+// depth-first order (the node, its reflection subtree, its transmission subtree) to give every
+// node the jitterIndex offset the depth-first render reaches there and the pixel its evaluation
+// count (k_jscan's input).  render_full and k_shade index the log the same way.
+
+// One node: walk its ray, log the hit, flag it, write its children (trace_full's EVENTS steps on
+// the same values: the same expressions, so the same rays).
+template <int WALK>
+__device__ __forceinline__ void level_node(const RenderParams& P, size_t q, int s, int h, int level, const V3& o,
+                                           const V3& d, double tlo, double time, Stack& st, Counts& c) {
+    const size_t S = (size_t)P.hit_stride;
+    const int b = P.hit_tree, per = P.tree_size;
+    const size_t at = (size_t)(s * per + h) * S + q;
+    Hit hh;
+    walk_closest<false, WALK>(P, o, d, rcp(d), tlo, time, hh, st, c);
+    DHitRec r;
+    r.t = hh.t; r.u = hh.u; r.v = hh.v; r.tri = hh.tri; r.inst = hh.inst;
+    P.hits[at] = r;
+    uint8_t fl = kNodeExists;
+    if (hh.inst >= 0) {
+        V3 p, Ngeo;
+        hit_geometry<false>(P, o, d, time, hh, p, Ngeo, c);
+        const DMaterial& M = P.mats[max(0, min(P.num_mats - 1, P.insts[hh.inst].material - 1))];
+        const bool frontFacing = dot(d, Ngeo) < 0;
+        const V3 N = frontFacing ? Ngeo : -Ngeo;
+        if (!(M.ior > 0) || frontFacing) fl |= kNodeEval;                 // computeDirect
+        auto spawn = [&](int which, const V3& co, const V3& cd) {
+            const size_t ca = (size_t)(s * per + tree_child(b, h, which)) * S + q;
+            DNodeRec& n = P.nodes[ca];
+            n.o[0] = co.x; n.o[1] = co.y; n.o[2] = co.z;
+            n.d[0] = cd.x; n.d[1] = cd.y; n.d[2] = cd.z;
+            n.time = time;
+            P.nflags[ca] = kNodeExists;
+        };
+        if (level < P.max_depth) {
+            if (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) {        // :189-206, :252-275
+                spawn(0, p + N * P.shadow_eps, normalize(reflect(d, N)));
+            } else if (M.type == RT_MAT_DIELECTRIC) {                          // :207-251
+                const bool entering = frontFacing;
+                const double n1 = entering ? 1.0 : M.ior;
+                const double n2 = entering ? M.ior : 1.0;
+                const double cosI = -dot(d, N);
+                double R, cosT, sin2T;
+                bool hasCosT;
+                fresnel_dielectric(n1, n2, cosI, R, hasCosT, cosT, sin2T);
+                const V3 rd = normalize(reflect(d, N));
+                spawn(0, p + rd * P.shadow_eps, rd);
+                if (!(!hasCosT || sin2T > 1)) {
+                    const double eta = n1 / n2;
+                    const V3 td = normalize((d * eta) + (N * (eta * cosI - cosT)));
+                    spawn(1, p + td * P.shadow_eps, td);
+                }
+            }
+        }
+    }
+    P.nflags[at] = fl;
+    P.nodes[at].hit = hh.inst >= 0 ? 1 : 0;
+}
+
+template <int WALK>
+__global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_level(RenderParams P, int level) {
+    extern __shared__ unsigned long long lds_stack[];
+    int i, j, slot, row;
+    full_pixel_of(P, i, j, slot, row);
+    if (i >= P.cam.width || j >= P.cam.height) return;
+    const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
+    Counts cnt{};
+    if (level > 0) {
+        const int width = P.hit_tree == 2 ? (1 << level) : 1;
+        const int s = (int)blockIdx.y / width, pos = (int)blockIdx.y % width;
+        const int h = (P.hit_tree == 2 ? (1 << level) - 1 : level) + pos;
+        const size_t at = (size_t)(s * P.tree_size + h) * (size_t)P.hit_stride + q;
+        if (!(P.nflags[at] & kNodeExists)) return;
+        MYRT_STACK(st, lds_stack);
+        const DNodeRec n = P.nodes[at];
+        level_node<WALK>(P, q, s, h, level, v3(n.o[0], n.o[1], n.o[2]), v3(n.d[0], n.d[1], n.d[2]), 0.0, n.time, st,
+                         cnt);
+        return;
+    }
+    // level 0: the pixel's primary rays, sample by sample, with pixel_full's draws
+    MYRT_STACK(st, lds_stack);
+    const DCamera& C = P.cam;
+    PCG32 rng((((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull);
+    const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
+    const int n = C.n;
+    int sampleIndex = 0;
+    for (int sy = 0; sy < n && sampleIndex < C.samples; ++sy) {
+        for (int sx = 0; sx < n; ++sx) {
+            const double xi1 = rng.nextFloat();
+            const double xi2 = rng.nextFloat();
+            const double currentI = (double)i + ((double)sx + xi1) / (double)n;
+            const double currentJ = (double)j + ((double)sy + xi2) / (double)n;
+            const V3 s = (q00 - v * (currentJ * C.dv)) + u * (currentI * C.du);
+            const V3 dir0 = normalize(s - eye);
+            V3 dir = dir0, camEye = eye;
+            if (C.aperture > 0 && C.focus > 0) {
+                const V3 forward = -w;
+                const double denom = dot(dir0, forward);
+                const double tFocus = fabs(denom) < 1e-6 ? C.focus : (C.focus / denom);
+                const V3 pFocus = eye + dir0 * tFocus;
+                const double uRand = rng.nextFloat() - 0.5;
+                const double vRand = rng.nextFloat() - 0.5;
+                const V3 lensOffset = ((uRand * u) + (vRand * v)) * C.aperture;
+                const V3 a = eye + lensOffset;
+                dir = normalize(pFocus - a);
+                camEye = a;
+            }
+            const double time = rng.nextFloat();
+            const double denom = dot(dir, w);
+            const double tImg = dot((eye - w * C.nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
+            const size_t at = (size_t)(sampleIndex * P.tree_size) * (size_t)P.hit_stride + q;
+            DNodeRec& nr = P.nodes[at];
+            nr.o[0] = camEye.x; nr.o[1] = camEye.y; nr.o[2] = camEye.z;
+            nr.d[0] = dir.x; nr.d[1] = dir.y; nr.d[2] = dir.z;
+            nr.time = time;
+            level_node<WALK>(P, q, sampleIndex, 0, 0, camEye, dir, smax(tImg, 0.0), time, st, cnt);
+            sampleIndex += 1;
+            if (sampleIndex >= C.samples) break;
+        }
+    }
+}
+
+// After the last level: each node's jitterIndex offset in trace()'s depth-first order, and the
+// pixel's area-light evaluations (k_events' outputs).  Flags only: no walks.
+__global__ __launch_bounds__(256) void k_jofs(RenderParams P) {
+    int i, j, slot, row;
+    full_pixel_of(P, i, j, slot, row);
+    if (i >= P.cam.width || j >= P.cam.height) return;
+    const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
+    const size_t S = (size_t)P.hit_stride;
+    const int b = P.hit_tree, per = P.tree_size, traced = P.hit_slots / P.tree_size;
+    const long long na = P.num_alights;
+    long long ev = 0;
+    for (int s = 0; s < traced; ++s) {
+        auto at = [&](int h) { return (size_t)(s * per + h) * S + q; };
+        auto exists = [&](int h) { return h < per && (P.nflags[at(h)] & kNodeExists); };
+        int h = 0;                                            // the root always exists
+        for (;;) {
+            P.nodes[at(h)].jofs = (int32_t)ev;
+            if (P.nflags[at(h)] & kNodeEval) ev += na;
+            int nx = -1;                                      // next node in preorder
+            if (exists(tree_child(b, h, 0))) nx = tree_child(b, h, 0);
+            else if (b == 2 && exists(tree_child(b, h, 1))) nx = tree_child(b, h, 1);
+            else if (b == 2) {
+                for (int c = h; c != 0;) {
+                    const int p = tree_parent(b, c);
+                    if ((c & 1) && exists(tree_child(b, p, 1))) { nx = tree_child(b, p, 1); break; }
+                    c = p;
+                }
+            }
+            if (nx < 0) break;
+            h = nx;
+        }
+    }
+    P.events[q] = ev;
+}
+
 // Node-parallel shading (after k_jscan): the direct light of every logged walk k that hit,
 // one lane per (pixel, k) - the same hit_geometry and direct_light as render_full on the same
 // ray and hit, with the jitterIndex the render pass reaches at that node (the pixel's prefix +
@@ -426,7 +604,7 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_shade(RenderParams P) {
     size_t q = 0;
     if (valid) {
         q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
-        valid = k < P.walks[q];
+        valid = P.hit_tree ? (P.nflags[(size_t)k * (size_t)P.hit_stride + q] & kNodeExists) != 0 : k < P.walks[q];
     }
     if (valid) {
         const size_t at = (size_t)k * (size_t)P.hit_stride + q;
@@ -499,6 +677,7 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void render_full(RenderParams P
         const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;   // packed selection index
         long long jitterIndex = P.num_alights > 0 ? P.jstart[q] : 0;
         HitLog hl{P.hits + q, (size_t)P.hit_stride, 0, P.hits ? P.hit_slots : 0};
+        hl.tree = P.hits ? P.hit_tree : 0;
         const V3 px = pixel_full<COUNT, false, DEEP, WALK>(P, i, j, jitterIndex, st, cnt, hl) / (double)P.cam.samples;
         const size_t o = out_row_of(P, j >> 3, row) * (size_t)P.cam.width + i;
         if (P.out_rgb) {

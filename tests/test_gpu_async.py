@@ -4,7 +4,7 @@ RayTracer.swift:115-131, 137-205; bench.py keeps RT_MAX_IN_FLIGHT frames in flig
 Each submitted render must deliver exactly the image and counts the synchronous rt_render_ex
 delivers (which is itself checked against the oracle, test_gpu_frames.py / test_gpu_parity.py),
 whatever else is in flight: different cameras and chunk selections at once, waits out of order,
-several replicas, and the scenes that stay in submission order (dielectrics, area lights).
+several replicas, and full trace() renders (dielectrics, area lights) on their slot streams.
 Errors: too many in flight (RT_ERR_BUSY), unknown or repeated tickets, pageable outputs."""
 import copy
 
@@ -84,19 +84,39 @@ def test_pipelined_frames_against_the_oracle():
     eng.close()
 
 
-def test_ordered_scenes_dielectric_and_area_light():
-    """Dielectrics / area lights take the full trace() kernel with per-replica scratch: their
-    submitted renders run in order on the replica's stream; results equal rt_render_ex."""
+@pytest.mark.parametrize("full_flights", ["0", "2", "4"])
+def test_full_trace_renders_in_flight(monkeypatch, full_flights):
+    """Dielectrics / area lights take the full trace() passes (render_full.h), whose scratch
+    (event counts, jitter prefixes, hit log, node records) belongs to a stream: submitted renders
+    take slot q % MYRT_FULL_FLIGHTS's stream and scratch, so up to that many overlap (0: all on
+    the replica's stream, in order).  Two cameras, chunk selections and glass at once, waits in
+    a ring; every frame equals rt_render_ex's."""
+    monkeypatch.setenv("MYRT_FULL_FLIGHTS", full_flights)
     from test_gpu_features import _area_scene
-    sc = _area_scene(96, 64)                                 # area lights + glass (render_full)
+    sc = _area_scene(96, 64)                                 # area lights (render_full)
+    sc.objects[3].material = "3"                             # + glass
+    c2 = copy.deepcopy(sc.cameras[0])
+    c2.position = (1.0, 1.5, 5.0)
+    sc.cameras.append(c2)
     W, H = sc.cameras[0].image_resolution
     eng = M.RayTracerEngine(sc)
-    want = _sync(eng, 0, 0, 1, H, W)
-    outs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(3)]
-    ts = [eng.submit_into(0, 0, 1, rgba=o, frame_layout=True) for o in outs]
-    for t, o in zip(ts, outs):
-        eng.wait(t)
-        assert np.array_equal(o, want[1])
+    jobs = [(0, 0, 1), (1, 0, 1), (0, 1, 3), (1, 2, 2)]
+    want = [_sync(eng, *j, H, W) for j in jobs]
+    Q = 6
+    outs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
+    pend = []
+    for k in range(3 * len(jobs)):
+        if len(pend) == Q:
+            kk, t = pend.pop(0)
+            st = eng.wait(t)
+            assert np.array_equal(outs[kk % Q], want[kk % len(jobs)][1])
+            assert st.shadow_rays == want[kk % len(jobs)][2].shadow_rays
+        outs[k % Q].fill(0)
+        pend.append((k, eng.submit_into(*jobs[k % len(jobs)], rgba=outs[k % Q], frame_layout=True)))
+    for kk, t in pend:
+        st = eng.wait(t)
+        assert np.array_equal(outs[kk % Q], want[kk % len(jobs)][1])
+        assert st.secondary_rays == want[kk % len(jobs)][2].secondary_rays
     eng.close()
 
 

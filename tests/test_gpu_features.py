@@ -137,6 +137,25 @@ def test_area_light_hit_log(monkeypatch, slots, nodeshade):
     assert st.secondary_rays > 0
 
 
+@pytest.mark.parametrize("levels", ["1", "0"])
+@pytest.mark.parametrize("spp, depth, glass", [(1, 4, True), (4, 3, True), (1, 5, True), (4, 4, False), (9, 2, True)])
+def test_area_light_level_passes(monkeypatch, levels, spp, depth, glass):
+    """Breadth-first events passes (render_full.h k_level, MYRT_LEVELS=1, default) against the
+    depth-first k_events (0): no rough material, so the tree's walks may run level by level;
+    heap-indexed trees with glass (2^(D+1) - 1 nodes per traced sample), chains without; 4 and 9
+    samples per pixel give several trees per pixel; depth 5 with one sample fills 63 of the 64
+    log slots.  k_jofs must reproduce the depth-first jitterIndex offsets exactly."""
+    monkeypatch.setenv("MYRT_LEVELS", levels)
+    monkeypatch.delenv("MYRT_HITLOG", raising=False)
+    sc = _area_scene(72, 56, spp=spp)
+    sc.objects[1].material = "3" if glass else "2"
+    sc.objects[2].material = "4"
+    sc.objects[3].material = "3" if glass else "4"
+    sc.max_recursion_depth = depth
+    st = _compare(sc)
+    assert st.secondary_rays > 0
+
+
 def test_c5_10m_mirrors_sampled_chunks_and_full_frame(scene_dir):
     """C5 (BASELINE configs[4]): ~10M triangles in two meshes (TLAS of 2), 3840x2160,
     depth-4 mirror reflections.  SURVEY.md §8d: 'for C5 check a sampled 1/64 of the rows
