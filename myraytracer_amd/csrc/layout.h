@@ -206,6 +206,7 @@ struct RenderParams {
     int32_t hit_tree;
     int32_t tree_size;
     uint8_t* nflags;
+    int32_t tree_ppw;                // node positions per wave in k_level / k_shade
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

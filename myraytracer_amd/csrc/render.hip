@@ -1190,6 +1190,10 @@ static bool scene_is_rough(const HostScene& S) {
 }
 // breadth-first events passes for area-light frames (render_full.h k_level; MYRT_LEVELS)
 constexpr int32_t kLevelsDefault = 1;
+// node positions of a tree level one wave of k_level / k_shade runs (MYRT_TREE_PPW): one per wave
+// dispatches mostly empty waves at the deep levels, all in one wave makes a tile's positions a
+// serial chain (the slowest tile bounds a pass)
+constexpr int32_t kTreePpwDefault = 4;
 static bool scene_has_bounce(const HostScene& S) {
     for (const auto& m : S.mats) if (m.type == RT_MAT_MIRROR || m.type == RT_MAT_CONDUCTOR) return true;
     return false;
@@ -1324,6 +1328,7 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
         }
         levels = levels && slots * px <= fs.nflags_cap;
         P.hit_tree = levels ? tree : 0;
+        P.tree_ppw = env_int("MYRT_TREE_PPW", kTreePpwDefault, 1, 64);
         P.tree_size = levels ? (int32_t)tree_size : 0;
         P.nflags = levels ? fs.nflags : nullptr;
         if (levels) {
@@ -1332,7 +1337,7 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
             const unsigned g0 = per_slot * (unsigned)P.num_chunks;
 #define MYRT_LV(W_) hipLaunchKernelGGL((dev::k_level<W_>), dim3(g0, ly, 1), block, lds, stream, P, level)
             for (int32_t level = 0; level <= P.max_depth; ++level) {
-                const unsigned ly = level == 0 ? 1u : (unsigned)traced * (tree == 2 ? (1u << level) : 1u);
+                const unsigned ly = level == 0 ? 1u : (unsigned)(traced * dev::tree_rows(tree, level, P.tree_ppw));
                 MYRT_BY_WALK(MYRT_LV);
             }
 #undef MYRT_LV
@@ -1350,8 +1355,11 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
         }
         hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), dim3(256, 1, 1), 0, stream, P);
         if (nodeshade) {
+            int64_t shade_rows = 0;                            // per traced sample (k_shade)
+            for (int32_t L = 0; P.hit_tree && L <= P.max_depth; ++L) shade_rows += dev::tree_rows(tree, L, P.tree_ppw);
             P.slot_base = 0;                                   // one launch over every chunk
-            const dim3 sgrid(per_slot * (unsigned)P.num_chunks, (unsigned)slots, 1);
+            const dim3 sgrid(per_slot * (unsigned)P.num_chunks,
+                             P.hit_tree ? (unsigned)(traced * shade_rows) : (unsigned)slots, 1);
 #define MYRT_SH(W_) hipLaunchKernelGGL((dev::k_shade<W_>), sgrid, block, lds, stream, P)
             MYRT_BY_WALK(MYRT_SH);
 #undef MYRT_SH

@@ -160,6 +160,11 @@ struct HitLog {
 enum : uint8_t { kNodeExists = 1, kNodeEval = 2 };
 __device__ __forceinline__ int tree_child(int b, int h, int which) { return b == 2 ? 2 * h + 1 + which : h + 1; }
 __device__ __forceinline__ int tree_parent(int b, int h) { return b == 2 ? (h - 1) >> 1 : h - 1; }
+// Level L of a tree: its first node and its width; a wave runs up to P.tree_ppw of its node
+// positions one after another (grid rows per level: tree_rows)
+__device__ __host__ __forceinline__ int tree_first(int b, int L) { return b == 2 ? (1 << L) - 1 : L; }
+__device__ __host__ __forceinline__ int tree_width(int b, int L) { return b == 2 ? (1 << L) : 1; }
+__device__ __host__ __forceinline__ int tree_rows(int b, int L, int ppw) { return (tree_width(b, L) + ppw - 1) / ppw; }
 
 template <bool COUNT, bool EVENTS, bool DEEP, int WALK>
 __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng,
@@ -497,15 +502,25 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_level(RenderParams P, in
     const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
     Counts cnt{};
     if (level > 0) {
-        const int width = P.hit_tree == 2 ? (1 << level) : 1;
-        const int s = (int)blockIdx.y / width, pos = (int)blockIdx.y % width;
-        const int h = (P.hit_tree == 2 ? (1 << level) - 1 : level) + pos;
-        const size_t at = (size_t)(s * P.tree_size + h) * (size_t)P.hit_stride + q;
-        if (!(P.nflags[at] & kNodeExists)) return;
+        // one wave per tile and traced sample runs the level's node positions one after another
+        // (a position's lanes are the same node of neighbouring pixels); a position no lane of
+        // the wave has is one flag load (launching one wave per position cost more in
+        // dispatching the empty ones than the walks)
+        const int rows = tree_rows(P.hit_tree, level, P.tree_ppw);
+        const int s = (int)blockIdx.y / rows, g = (int)blockIdx.y % rows;
+        const int width = min(P.tree_ppw, tree_width(P.hit_tree, level) - g * P.tree_ppw);
+        const int h0 = tree_first(P.hit_tree, level) + g * P.tree_ppw;
         MYRT_STACK(st, lds_stack);
-        const DNodeRec n = P.nodes[at];
-        level_node<WALK>(P, q, s, h, level, v3(n.o[0], n.o[1], n.o[2]), v3(n.d[0], n.d[1], n.d[2]), 0.0, n.time, st,
-                         cnt);
+        for (int pos = 0; pos < width; ++pos) {
+            const size_t at = (size_t)(s * P.tree_size + h0 + pos) * (size_t)P.hit_stride + q;
+            const bool ex = (P.nflags[at] & kNodeExists) != 0;
+            if (!__any(ex)) continue;
+            if (ex) {
+                const DNodeRec n = P.nodes[at];
+                level_node<WALK>(P, q, s, h0 + pos, level, v3(n.o[0], n.o[1], n.o[2]), v3(n.d[0], n.d[1], n.d[2]),
+                                 0.0, n.time, st, cnt);
+            }
+        }
         return;
     }
     // level 0: the pixel's primary rays, sample by sample, with pixel_full's draws
@@ -592,45 +607,61 @@ __global__ __launch_bounds__(256) void k_jofs(RenderParams P) {
 // the node's offset, both counted by k_events).  Grid: (the selection's tiles, hit_slots).
 // render_full then shades no logged hit itself: its waves no longer run the shadow walks of the
 // longest path tree with the other lanes idle.
+// One logged walk k of pixel q that hit: its direct light into node_lo.
+template <int WALK>
+__device__ __forceinline__ void shade_node(const RenderParams& P, size_t q, int k, Stack& st, Counts& cnt) {
+    const size_t at = (size_t)k * (size_t)P.hit_stride + q;
+    const DNodeRec n = P.nodes[at];
+    if (!n.hit) return;
+    const DHitRec r = P.hits[at];
+    Hit h;
+    h.t = r.t; h.u = r.u; h.v = r.v; h.tri = r.tri; h.inst = r.inst;
+    const V3 o = v3(n.o[0], n.o[1], n.o[2]), d = v3(n.d[0], n.d[1], n.d[2]);
+    V3 p, Ngeo;
+    hit_geometry<false>(P, o, d, n.time, h, p, Ngeo, cnt);
+    const int hitmat = P.insts[h.inst].material;
+    const int mi = max(0, min(P.num_mats - 1, hitmat - 1));
+    const DMaterial& M = P.mats[mi];
+    const bool frontFacing = dot(d, Ngeo) < 0;
+    const V3 N = frontFacing ? Ngeo : -Ngeo;
+    const bool computeDirect = !(M.ior > 0) || frontFacing;
+    V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+    if (computeDirect) {
+        long long jitterIndex = P.jstart[q] + n.jofs;
+        direct_light<false, WALK>(P, M, N, p, d, n.time, jitterIndex, st, cnt, Lo);
+    }
+    double* lo = P.node_lo + 3 * at;
+    lo[0] = Lo.x; lo[1] = Lo.y; lo[2] = Lo.z;
+}
+
+// Grid (the selection's tiles, hit_slots) for the k-th walk log; with tree-indexed logs
+// (hit_tree) grid (tiles, traced samples x tree levels), one wave running the level's node
+// positions one after another (as k_level).
 template <int WALK>
 __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_shade(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
-    const int k = (int)blockIdx.y;
     const int lane = threadIdx.x & 63;
     Counts cnt{};
-    bool valid = (i < P.cam.width) && (j < P.cam.height);
-    size_t q = 0;
-    if (valid) {
-        q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
-        valid = P.hit_tree ? (P.nflags[(size_t)k * (size_t)P.hit_stride + q] & kNodeExists) != 0 : k < P.walks[q];
+    const bool valid = (i < P.cam.width) && (j < P.cam.height);
+    const size_t q = valid ? ((size_t)slot * 8 + row) * (size_t)P.cam.width + i : 0;
+    MYRT_STACK(st, lds_stack);
+    int k0 = (int)blockIdx.y, width = 1;                    // log entries k0 .. k0 + width - 1
+    if (P.hit_tree) {                                       // row -> (sample, level, group)
+        int per = 0;
+        for (int L = 0; L <= P.max_depth; ++L) per += tree_rows(P.hit_tree, L, P.tree_ppw);
+        const int s = (int)blockIdx.y / per;
+        int r = (int)blockIdx.y % per, level = 0;
+        while (r >= tree_rows(P.hit_tree, level, P.tree_ppw)) r -= tree_rows(P.hit_tree, level++, P.tree_ppw);
+        width = min(P.tree_ppw, tree_width(P.hit_tree, level) - r * P.tree_ppw);
+        k0 = s * P.tree_size + tree_first(P.hit_tree, level) + r * P.tree_ppw;
     }
-    if (valid) {
-        const size_t at = (size_t)k * (size_t)P.hit_stride + q;
-        const DNodeRec n = P.nodes[at];
-        if (n.hit) {
-            MYRT_STACK(st, lds_stack);
-            const DHitRec r = P.hits[at];
-            Hit h;
-            h.t = r.t; h.u = r.u; h.v = r.v; h.tri = r.tri; h.inst = r.inst;
-            const V3 o = v3(n.o[0], n.o[1], n.o[2]), d = v3(n.d[0], n.d[1], n.d[2]);
-            V3 p, Ngeo;
-            hit_geometry<false>(P, o, d, n.time, h, p, Ngeo, cnt);
-            const int hitmat = P.insts[h.inst].material;
-            const int mi = max(0, min(P.num_mats - 1, hitmat - 1));
-            const DMaterial& M = P.mats[mi];
-            const bool frontFacing = dot(d, Ngeo) < 0;
-            const V3 N = frontFacing ? Ngeo : -Ngeo;
-            const bool computeDirect = !(M.ior > 0) || frontFacing;
-            V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
-            if (computeDirect) {
-                long long jitterIndex = P.jstart[q] + n.jofs;
-                direct_light<false, WALK>(P, M, N, p, d, n.time, jitterIndex, st, cnt, Lo);
-            }
-            double* lo = P.node_lo + 3 * at;
-            lo[0] = Lo.x; lo[1] = Lo.y; lo[2] = Lo.z;
-        }
+    for (int k = k0; k < k0 + width; ++k) {                 // one call site of the shadow walk
+        const bool ex = valid && (P.hit_tree ? (P.nflags[(size_t)k * (size_t)P.hit_stride + q] & kNodeExists) != 0
+                                             : k < P.walks[q]);
+        if (!__any(ex)) continue;
+        if (ex) shade_node<WALK>(P, q, k, st, cnt);
     }
     const unsigned long long s0 = wave_sum(cnt.shadow), s2 = wave_sum(cnt.shadow_traced);
     if (lane == 0) {

@@ -137,15 +137,17 @@ def test_area_light_hit_log(monkeypatch, slots, nodeshade):
     assert st.secondary_rays > 0
 
 
-@pytest.mark.parametrize("levels", ["1", "0"])
+@pytest.mark.parametrize("levels, ppw", [("1", "4"), ("1", "1"), ("1", "64"), ("0", "4")])
 @pytest.mark.parametrize("spp, depth, glass", [(1, 4, True), (4, 3, True), (1, 5, True), (4, 4, False), (9, 2, True)])
-def test_area_light_level_passes(monkeypatch, levels, spp, depth, glass):
+def test_area_light_level_passes(monkeypatch, levels, ppw, spp, depth, glass):
     """Breadth-first events passes (render_full.h k_level, MYRT_LEVELS=1, default) against the
     depth-first k_events (0): no rough material, so the tree's walks may run level by level;
     heap-indexed trees with glass (2^(D+1) - 1 nodes per traced sample), chains without; 4 and 9
     samples per pixel give several trees per pixel; depth 5 with one sample fills 63 of the 64
-    log slots.  k_jofs must reproduce the depth-first jitterIndex offsets exactly."""
+    log slots.  k_jofs must reproduce the depth-first jitterIndex offsets exactly.  A wave runs 1,
+    4 (default) or all of a level's node positions (MYRT_TREE_PPW)."""
     monkeypatch.setenv("MYRT_LEVELS", levels)
+    monkeypatch.setenv("MYRT_TREE_PPW", ppw)
     monkeypatch.delenv("MYRT_HITLOG", raising=False)
     sc = _area_scene(72, 56, spp=spp)
     sc.objects[1].material = "3" if glass else "2"
