@@ -446,6 +446,9 @@ __device__ __forceinline__ bool inner_step_rec(const RenderParams& P, const Rec&
 // at the same node.  Vector loads of one node by 64 lanes return 64 copies through the
 // texture-data path (7 instructions x 1 KB per wave step), which profiling showed ~90%
 // busy (TD_TD_BUSY); the scalar path moves the 104 B once, through the scalar cache.
+#ifndef MYRT_SCALAR_COMPACT
+#define MYRT_SCALAR_COMPACT 1   // wave-uniform steps on compact BLAS records read them (16 SGPRs, not 26)
+#endif
 struct SRec {
     double lo[2][3], hi[2][3];
     int ref[2];
@@ -481,8 +484,26 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
     if (__all(ref == r0)) {
         if (COUNT && !P.count_ref)
             c.it_wave_scalar[SHADOW] += ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) ? 1 : 0;
-        // the wave-uniform step reads the FP64 record (no v_cvt_f64_f32; C3/C5 -0.5 % against
-        // the compact record through SGPRs)
+        // The wave-uniform step reads the compact record when there is one: 16 SGPRs instead of
+        // the FP64 record's 26 leave the walk loop fewer spilled SGPRs to restore at its back
+        // edge (C3 -0.3 %, pipelined -0.46 %, C5 -0.6 %; profiles/r03t_ab_scalar_compact.txt),
+        // though each step then converts 12 bounds (in round 2, before the register-allocation
+        // changes since, the FP64 record had measured 0.5 % faster).
+#if MYRT_SCALAR_COMPACT
+        if (r0 < P.compact_limit) {          // the compact record: 16 SGPRs instead of 26
+            const unsigned long long av = (unsigned long long)(P.crecs + r0);
+            const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
+            const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
+            typedef const __attribute__((address_space(4))) CRec c4_crec;
+            c4_crec* p = (c4_crec*)((unsigned long long)alo | ((unsigned long long)ahi << 32));
+            CRec R;
+            for (int k = 0; k < 2; ++k)
+                for (int a = 0; a < 3; ++a) { R.lo[k][a] = p->lo[k][a]; R.hi[k][a] = p->hi[k][a]; }
+            R.ref[0] = p->ref[0];
+            R.ref[1] = p->ref[1];
+            return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
+        }
+#endif
         const SRec R = load_rec_scalar(P.recs + r0);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
     }
