@@ -70,7 +70,7 @@ def parse():
     # 2000 C3 frames = ~1.3 s timed at N = 1: long enough for an outside GPU-busy sampler
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--config", default="c3", choices=["c2", "c3", "c5", "c3i", "c3g"],
+    p.add_argument("--config", default="c3", choices=["c2", "c3", "c5", "c3i", "c3g", "c3d"],
                    help="c3 (default, BASELINE configs[2]); c2 / c5 (configs[1] / [4]); c3i: C3 as 25 mesh "
                         "instances with transforms (literal TLAS->BLAS walk); c3g: C3 with glass spheres and two "
                         "area lights (full trace() kernels)")
@@ -185,6 +185,10 @@ def main():
         scene = scenes.scene_c3_instanced(path_dir=args.cache)
         workload = ("C3i: C3's geometry as 25 mesh instances with non-identity transforms (terrain + 24 instances "
                     "of one icosphere BLAS), 1920x1080, 1 spp, 1 point light, shadows: the literal TLAS->BLAS walk")
+    elif args.config == "c3d":
+        scene = scenes.scene_c3_glass(path_dir=args.cache, area_lights=False)
+        workload = ("C3d: C3's geometry with 24 glass (dielectric, Beer) spheres, 1 point light, "
+                    "1920x1080, 1 spp, maxRecursionDepth 4: level passes + node shading + render_full")
     elif args.config == "c3g":
         scene = scenes.scene_c3_glass(path_dir=args.cache)
         workload = ("C3g: C3's geometry with 24 glass (dielectric, Beer) spheres, 1 point + 2 area lights, "

@@ -1264,15 +1264,24 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
         else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
         else M_(dev::kWalkGeneral);                                         \
     } while (0)
-    if (P.num_alights > 0) {
+    // Area-light frames need the events passes (jitterIndex prefixes); dielectric frames without
+    // area lights take the same level passes + node shading when they apply (no rough
+    // material, whole trees logged), else render_full alone walks and shades every tree.
+    const bool alights = P.num_alights > 0;
+    if (alights || (dielectric && !count && !deep)) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
         if (px > fs.cap_px) {
             (void)hipFree(fs.events); (void)hipFree(fs.jstart);
             fs.events = nullptr; fs.jstart = nullptr; fs.cap_px = 0;
             if (hipMalloc((void**)&fs.events, px * sizeof(long long)) != hipSuccess ||
-                hipMalloc((void**)&fs.jstart, px * sizeof(long long)) != hipSuccess)
-                return fail(RT_ERR_OOM, "device allocation of area-light jitter buffers failed");
-            fs.cap_px = px;
+                hipMalloc((void**)&fs.jstart, px * sizeof(long long)) != hipSuccess) {
+                (void)hipFree(fs.events); (void)hipFree(fs.jstart);
+                fs.events = nullptr; fs.jstart = nullptr;
+                if (alights) return fail(RT_ERR_OOM, "device allocation of area-light jitter buffers failed");
+                (void)hipGetLastError();
+            } else {
+                fs.cap_px = px;
+            }
         }
         P.events = fs.events;
         P.jstart = fs.jstart;
@@ -1326,7 +1335,12 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
             if (hipMalloc((void**)&fs.nflags, (size_t)(slots * px)) == hipSuccess) fs.nflags_cap = slots * px;
             else (void)hipGetLastError();             // depth-first k_events
         }
-        levels = levels && slots * px <= fs.nflags_cap;
+        levels = levels && slots * px <= fs.nflags_cap && px <= fs.cap_px;
+        if (!alights && !levels) {                     // dielectrics only: render_full does it all
+            P.hits = nullptr; P.hit_slots = 0;
+            P.nodes = nullptr; P.node_lo = nullptr; P.walks = nullptr;
+            nodeshade = false;
+        }
         P.hit_tree = levels ? tree : 0;
         P.tree_ppw = env_int("MYRT_TREE_PPW", kTreePpwDefault, 1, 64);
         P.tree_size = levels ? (int32_t)tree_size : 0;
@@ -1343,7 +1357,7 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
 #undef MYRT_LV
             hipLaunchKernelGGL(dev::k_jofs, dim3(g0), block, 0, stream, P);
         }
-        for (int32_t base = 0; base < P.num_chunks && !levels; base += batch) {
+        for (int32_t base = 0; base < P.num_chunks && !levels && alights; base += batch) {
             P.slot_base = base;
             dim3 grid(per_slot * (unsigned)std::min(batch, P.num_chunks - base), 1, 1);
 #define MYRT_EV1(W_) hipLaunchKernelGGL((dev::k_events<true, W_>), grid, block, lds, stream, P)
@@ -1353,7 +1367,7 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
 #undef MYRT_EV1
 #undef MYRT_EV0
         }
-        hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), dim3(256, 1, 1), 0, stream, P);
+        if (alights) hipLaunchKernelGGL(dev::k_jscan, dim3((unsigned)P.num_chunks), dim3(256, 1, 1), 0, stream, P);
         if (nodeshade) {
             int64_t shade_rows = 0;                            // per traced sample (k_shade)
             for (int32_t L = 0; P.hit_tree && L <= P.max_depth; ++L) shade_rows += dev::tree_rows(tree, L, P.tree_ppw);

@@ -627,7 +627,7 @@ __device__ __forceinline__ void shade_node(const RenderParams& P, size_t q, int 
     const bool computeDirect = !(M.ior > 0) || frontFacing;
     V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
     if (computeDirect) {
-        long long jitterIndex = P.jstart[q] + n.jofs;
+        long long jitterIndex = (P.num_alights > 0 ? P.jstart[q] : 0) + n.jofs;
         direct_light<false, WALK>(P, M, N, p, d, n.time, jitterIndex, st, cnt, Lo);
     }
     double* lo = P.node_lo + 3 * at;

@@ -304,11 +304,13 @@ def scene_c3_instanced(path_dir: str = None, width: int = 1920, height: int = 10
                  max_recursion_depth=4)
 
 
-def scene_c3_glass(path_dir: str = None, width: int = 1920, height: int = 1080, inline: bool = False) -> Scene:
+def scene_c3_glass(path_dir: str = None, width: int = 1920, height: int = 1080, inline: bool = False,
+                   area_lights: bool = True) -> Scene:
     """C3's geometry with the 24 spheres made of glass (dielectric with Beer absorption, two
     child rays per bounce, Object+Extension.swift:207-251) and two area lights next to the
     point light (:145-186, the chunk-sequential jitterIndex): the full trace() kernels
-    (render_full, k_events + k_jscan).  Terrain and spheres are two meshes, maxRecursionDepth 4."""
+    (render_full, k_events + k_jscan).  Terrain and spheres are two meshes, maxRecursionDepth 4.
+    area_lights=False: the point light alone (C3d: dielectric paths without the events passes)."""
     seed = 42
     hp, hf = heightfield(512, 100.0, 6.0, seed)
     rng = np.random.RandomState(seed + 1)
@@ -331,7 +333,7 @@ def scene_c3_glass(path_dir: str = None, width: int = 1920, height: int = 1080, 
                  area_lights=[AreaLight(position=(-20.0, 30.0, 10.0), normal=(0.5, -1.0, -0.2), radiance=(900.0, 850.0, 800.0),
                                         size=4.0),
                               AreaLight(position=(25.0, 20.0, -10.0), normal=(-1.0, -0.6, 0.3),
-                                        radiance=(300.0, 400.0, 600.0), size=3.0)],
+                                        radiance=(300.0, 400.0, 600.0), size=3.0)] if area_lights else [],
                  ambient_light=(15.0, 15.0, 15.0), background_color=(40.0, 60.0, 90.0), shadow_ray_epsilon=1e-3,
                  intersection_test_epsilon=1e-6, max_recursion_depth=4)
 

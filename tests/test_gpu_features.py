@@ -158,6 +158,22 @@ def test_area_light_level_passes(monkeypatch, levels, ppw, spp, depth, glass):
     assert st.secondary_rays > 0
 
 
+@pytest.mark.parametrize("levels", ["1", "0"])
+@pytest.mark.parametrize("spp, depth", [(1, 4), (4, 3)])
+def test_dielectric_level_passes_without_area_lights(monkeypatch, levels, spp, depth):
+    """Glass + mirror + conductor with point lights only: the level passes and node shading
+    (MYRT_LEVELS=1, default) or render_full alone (0).  No jitterIndex here, so no events prefix."""
+    monkeypatch.setenv("MYRT_LEVELS", levels)
+    monkeypatch.delenv("MYRT_HITLOG", raising=False)
+    sc = _primitives_scene(80, 60)
+    sc.cameras[0].num_samples = spp
+    sc.objects[1].material = "3"
+    sc.objects[3].material = "3"
+    sc.max_recursion_depth = depth
+    st = _compare(sc)
+    assert st.secondary_rays > 0
+
+
 def test_c5_10m_mirrors_sampled_chunks_and_full_frame(scene_dir):
     """C5 (BASELINE configs[4]): ~10M triangles in two meshes (TLAS of 2), 3840x2160,
     depth-4 mirror reflections.  SURVEY.md §8d: 'for C5 check a sampled 1/64 of the rows

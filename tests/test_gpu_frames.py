@@ -225,15 +225,17 @@ def test_bench_strong_split_eight_ranks_on_one_gpu():
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("name", ["c3i", "c3g"])
+@pytest.mark.parametrize("name", ["c3i", "c3g", "c3d"])
 def test_general_path_bench_configs_full_frame(scene_dir, name, monkeypatch):
     """The bench's general-path configs on full 1920x1080 frames against the oracle: C3i (C3's
     geometry as 25 transformed mesh instances: the literal TLAS->BLAS walk, RTContext.swift:
     619-720) and C3g (glass spheres + two area lights: render_full with k_events/k_jscan,
-    Object+Extension.swift:145-251), through bench.py's call (RGBA8 into page-locked memory)
-    and the FP64 frame."""
+    Object+Extension.swift:145-251) and C3d (the glass spheres with the point light only: level
+    passes + node shading without events), through bench.py's call (RGBA8 into page-locked
+    memory) and the FP64 frame."""
     monkeypatch.delenv("MYRT_PATH", raising=False)
-    make = {"c3i": scenes.scene_c3_instanced, "c3g": scenes.scene_c3_glass}[name]
+    make = {"c3i": scenes.scene_c3_instanced, "c3g": scenes.scene_c3_glass,
+            "c3d": lambda path_dir: scenes.scene_c3_glass(path_dir=path_dir, area_lights=False)}[name]
     sc = make(path_dir=scene_dir)
     ref, ref8, ost = oracle.OracleScene(_inline(sc)).render(0, threads=0, rgba=True)
     eng = M.RayTracerEngine(sc)
