@@ -1,0 +1,16 @@
+set -u
+T=r03w
+bash tools/prof_session.sh ${T}_c3 || exit $?
+bash tools/prof_session.sh ${T}_c5 --config c5 || exit $?
+bash tools/overlap_session.sh ${T}_c3 c3 300 || exit $?
+bash tools/overlap_session.sh ${T}_c5 c5 100 || exit $?
+bash tools/gpu_session.sh \
+ "${T}_smoke|300|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
+ "${T}_bc3|300|python3 bench.py > gpurun_out/${T}_bench_c3.json" \
+ "${T}_bc5|300|python3 bench.py --config c5 --steps 400 --warmup 20 --no-cpu-baseline > gpurun_out/${T}_bench_c5.json" \
+ "${T}_bc3i|300|python3 bench.py --config c3i --steps 400 --warmup 20 --no-cpu-baseline > gpurun_out/${T}_bench_c3i.json" \
+ "${T}_bc3g|300|python3 bench.py --config c3g --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_bench_c3g.json" \
+ "${T}_bc3g_trace|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_c3g_trace -- python3 bench.py --config c3g --steps 10 --warmup 2 --in-flight 1 --no-cpu-baseline --no-side-paths"
+bash tools/gpu_session.sh \
+ "${T}_bc3d|300|python3 bench.py --config c3d --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_bench_c3d.json" \
+ "${T}_suite|700|python -u -m pytest -x -v --timeout 400 --timeout-method thread tests -m gpu"
