@@ -446,6 +446,9 @@ __device__ __forceinline__ bool inner_step_rec(const RenderParams& P, const Rec&
 // at the same node.  Vector loads of one node by 64 lanes return 64 copies through the
 // texture-data path (7 instructions x 1 KB per wave step), which profiling showed ~90%
 // busy (TD_TD_BUSY); the scalar path moves the 104 B once, through the scalar cache.
+#ifndef MYRT_SCALAR_FULL
+#define MYRT_SCALAR_FULL 1      // wave-uniform steps on full (FP64) records through SGPRs too (A/B)
+#endif
 #ifndef MYRT_SCALAR_COMPACT
 #define MYRT_SCALAR_COMPACT 1   // wave-uniform steps on compact BLAS records read them (16 SGPRs, not 26)
 #endif
@@ -504,8 +507,10 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
             return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
         }
 #endif
+#if MYRT_SCALAR_FULL
         const SRec R = load_rec_scalar(P.recs + r0);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
+#endif
     }
     if (COUNT && !P.count_ref) {             // redundancy of the per-lane loads below
         unsigned long long left = __ballot(1);
