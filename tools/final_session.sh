@@ -1,3 +1,8 @@
+#!/usr/bin/env bash
+# The round's final measurement session (run on the GPU box via gpurun): PMC + kernel-trace
+# profiles of C3/C5 (tools/prof_session.sh), the bench loop's kernel overlap
+# (tools/overlap_session.sh), smoke, bench lines of every config and the GPU suite.
+# usage: gpurun -- 'bash tools/final_session.sh'  ->  gpurun_out/r03w_*
 set -u
 T=r03w
 bash tools/prof_session.sh ${T}_c3 || exit $?
