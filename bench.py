@@ -73,7 +73,7 @@ def parse():
     p.add_argument("--config", default="c3", choices=["c2", "c3", "c5", "c3i", "c3g", "c3d"],
                    help="c3 (default, BASELINE configs[2]); c2 / c5 (configs[1] / [4]); c3i: C3 as 25 mesh "
                         "instances with transforms (literal TLAS->BLAS walk); c3g: C3 with glass spheres and two "
-                        "area lights (full trace() kernels)")
+                        "area lights (full trace() kernels); c3d: the glass spheres with the point light only")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong (default): one frame per step split over the ranks (C4); "
                         "weak: every rank renders a full frame per step")
