@@ -66,6 +66,7 @@ struct RenderStats {                                    /* Models/RenderStats.sw
     int64_t rays = 0;                                   /* primary + shadow */
     int64_t primary_rays = 0, shadow_rays = 0, secondary_rays = 0;
     int64_t shadow_rays_traced = 0;                     /* any-hit walks that ran (<= shadow_rays) */
+    int64_t rewalked = 0;                               /* closest-hit rays re-walked in reference order (ties) */
     double milliseconds = 0, kernel_ms = 0;
 };
 
@@ -131,6 +132,14 @@ public:
     }
 
     rt_scene* handle() const { return scene_; }
+
+    /* Render options (rt_scene_set_option; defaults are the production settings). */
+    void setOption(const std::string& name, int64_t value) { check(rt_scene_set_option(scene_, name.c_str(), value)); }
+    int64_t option(const std::string& name) const {
+        int64_t v = 0;
+        check(rt_scene_get_option(scene_, name.c_str(), &v));
+        return v;
+    }
 
 private:
     static int32_t fileFormat(SceneFormat f) {
@@ -247,6 +256,7 @@ private:
         r.rays = st.primary_rays + st.shadow_rays;
         r.milliseconds = st.milliseconds; r.kernel_ms = st.kernel_ms;
         r.shadow_rays_traced = st.shadow_rays_traced;
+        r.rewalked = st.rewalked;
         return r;
     }
     rt_scene* scene_ = nullptr;

@@ -44,8 +44,11 @@
  *   2: rt_object gained `num_normals` (sizeof(rt_object), the stride of rt_scene_desc.objects,
  *      changed: callers built against version 1 must be rebuilt).  A non-NULL `normals` now
  *      requires num_normals == num_positions; version-1 callers that left it 0 get
- *      RT_ERR_INVALID_ARG instead of an unchecked read. */
-#define RT_ABI_VERSION 2
+ *      RT_ERR_INVALID_ARG instead of an unchecked read.
+ *   3: rt_stats gained `rewalked` and rt_scene_info `scratch_bytes` (both appended: the
+ *      structs grew); rt_scene_set_option / rt_scene_get_option replace the MYRT_*
+ *      environment switches (the library reads no environment variable on the render path). */
+#define RT_ABI_VERSION 3
 
 #ifdef __cplusplus
 extern "C" {
@@ -165,6 +168,8 @@ typedef struct rt_stats {       /* RenderStats (Models/RenderStats.swift:8-24) +
     int64_t shadow_rays_traced; /* shadow rays whose any-hit walk actually ran: the walk is
                                  * skipped when !(N.L > 0), where the reference discards the
                                  * occlusion result (Object+Extension.swift:123-141)      */
+    int64_t rewalked;           /* closest-hit rays the four-wide walk handed to the reference-
+                                 * order walk because two candidates met their final t    */
 } rt_stats;
 
 typedef struct rt_scene_info {
@@ -173,6 +178,8 @@ typedef struct rt_scene_info {
     double  build_ms;           /* PLY load + flatten + BVH build + layout            */
     double  upload_ms;          /* host -> device copies                               */
     int64_t device_bytes;       /* per-device resident scene bytes                     */
+    int64_t scratch_bytes;      /* device scratch held now by replica 0 (render outputs, pass
+                                 * scratch of full trace() renders, queues, deep frames) */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene;   /* opaque */
@@ -187,6 +194,24 @@ int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32
                         rt_scene** out);
 void    rt_scene_destroy(rt_scene* scene);
 int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
+
+/* Render options: tuning and test switches, each default being the production setting.
+ *   wide (1)             conservative FP32 four-wide walk of identity scenes (exact: wide.h)
+ *   unified (1)          one-stack TLAS+BLAS walks; 0 = the nested walk of intersectTLAS
+ *   unified_transformed (1)  one-stack walk of instanced scenes (device.h ut_walk)
+ *   compact_records (1), compact_tris (1)   float32 records / triangles when exact
+ *   xcd_group (0 = auto) tiles per XCD run      queue (0)  compacted bounce render
+ *   queue_levels (-1)    timing probe           hitlog (-1 = auto) logged hits per pixel
+ *   nodeshade (1), levels (1), tree_ppw (4)     full trace() pass structure
+ *   full_flights (4)     full trace() renders overlapping on slot streams
+ *   deep_cap_mb (8192)   deep trace() frames per launch batch
+ *   batches (0 = auto), zerocopy (1)            rt_render delivery
+ *   submit_events (1), submit_counters (1), submit_dma (0)   rt_render_submit delivery
+ *   debug_fail_replica (-1)   test hook: inject a launch failure on that replica
+ * Unknown names and out-of-range values return RT_ERR_INVALID_ARG.  Set options between
+ * renders (not while renders of the scene are in flight). */
+int32_t rt_scene_set_option(rt_scene* scene, const char* name, int64_t value);
+int32_t rt_scene_get_option(const rt_scene* scene, const char* name, int64_t* value);
 
 /* ---- rendering -------------------------------------------------------------- */
 /* Renders 8-row chunks chunk_first, chunk_first+chunk_step, ... of camera
@@ -243,8 +268,11 @@ int32_t rt_host_unregister(void* ptr);
 
 /* Same as rt_render on ONE device slot, but outputs are DEVICE pointers on that
  * device and the work is enqueued on `stream` (a hipStream_t, NULL = default)
- * without host synchronisation.  Ray counters (if stats != NULL) are only valid
- * after rt_stats_collect() once the stream has drained. */
+ * without host synchronisation.  Ray counters are only valid after rt_stats_collect()
+ * once the stream has drained.  Device renders have their own counters, pass scratch and
+ * queues, so they may overlap rt_render / rt_render_submit renders of the same scene;
+ * exception: scenes with maxRecursionDepth > 16 share one deep-frame buffer per replica,
+ * and a device render of such a scene must not overlap another render of it. */
 int32_t rt_render_device(rt_scene* scene, int32_t device_slot, int32_t camera_index,
                          int32_t chunk_first, int32_t chunk_step,
                          double* d_out_rgb, uint8_t* d_out_rgba8, void* stream);

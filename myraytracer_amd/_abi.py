@@ -69,14 +69,14 @@ class rt_stats(C.Structure):
     _fields_ = [("meshes", C.c_int64), ("triangles", C.c_int64), ("spheres", C.c_int64), ("planes", C.c_int64),
                 ("primary_rays", C.c_int64), ("shadow_rays", C.c_int64), ("secondary_rays", C.c_int64),
                 ("milliseconds", C.c_double), ("kernel_ms", C.c_double),
-                ("shadow_rays_traced", C.c_int64)]
+                ("shadow_rays_traced", C.c_int64), ("rewalked", C.c_int64)]
 
 
 class rt_scene_info(C.Structure):
     _fields_ = [("meshes", C.c_int64), ("triangles", C.c_int64), ("spheres", C.c_int64), ("planes", C.c_int64),
                 ("instances", C.c_int64), ("blas_nodes", C.c_int64), ("tlas_nodes", C.c_int64),
                 ("max_depth", C.c_int64), ("build_ms", C.c_double), ("upload_ms", C.c_double),
-                ("device_bytes", C.c_int64)]
+                ("device_bytes", C.c_int64), ("scratch_bytes", C.c_int64)]
 
 
 class rt_work_counters(C.Structure):
@@ -130,8 +130,9 @@ EXPORTED_SYMBOLS = [
     "rt_debug_rcp", "rt_render_submit", "rt_render_wait",
     "rt_render_ex", "rt_host_register", "rt_host_unregister",
     "rt_scene_file_load", "rt_scene_file_parse", "rt_scene_file_desc", "rt_scene_file_image_name",
-    "rt_scene_file_last_error", "rt_scene_file_destroy",
+    "rt_scene_file_last_error", "rt_scene_file_destroy", "rt_scene_set_option", "rt_scene_get_option",
 ]
+RT_ABI_VERSION = 3
 
 
 def bind(lib: C.CDLL) -> C.CDLL:
@@ -207,4 +208,9 @@ def bind(lib: C.CDLL) -> C.CDLL:
     lib.rt_debug_occluded_rays.argtypes = [C.c_void_p, C.c_int32, C.c_int32, c_double_p, c_double_p, c_double_p,
                                            c_double_p, P(C.c_uint8)]
     lib.rt_debug_occluded_rays.restype = C.c_int32
+    if hasattr(lib, "rt_scene_set_option"):   # ABI >= 3 (an older build may be loaded for an A/B, MYRT_LIB)
+        lib.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+        lib.rt_scene_set_option.restype = C.c_int32
+        lib.rt_scene_get_option.argtypes = [C.c_void_p, C.c_char_p, P(C.c_int64)]
+        lib.rt_scene_get_option.restype = C.c_int32
     return lib

@@ -17,7 +17,7 @@ PKG = os.path.join(ROOT, "myraytracer_amd")
 CSRC = os.path.join(PKG, "csrc")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
-PRODUCT_SOURCES = ["render.hip", "wavefront.hip", "scene.cpp", "ply.cpp", "sceneio.cpp"]
+PRODUCT_SOURCES = ["render.hip", "scene.cpp", "ply.cpp", "sceneio.cpp"]
 # -ffp-contract=off on host AND device: the reference does no FMA contraction
 COMMON_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
 
@@ -37,7 +37,7 @@ def _stale(target, sources):
 def build_product(force: bool = False) -> str:
     out = os.path.join(PKG, "libmyrt.so")
     srcs = [os.path.join(CSRC, s) for s in PRODUCT_SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in ("layout.h", "scene.h", "device.h", "wavefront.h", "render_full.h")] + [os.path.join(ROOT, "include", "rtcore.h")]
+    deps = srcs + [os.path.join(CSRC, h) for h in ("layout.h", "scene.h", "device.h", "wide.h", "render_full.h")] + [os.path.join(ROOT, "include", "rtcore.h")]
     if force or _stale(out, deps):
         _run([HIPCC, "--offload-arch=gfx950", *COMMON_FLAGS, "-o", out, *srcs])
     return out

@@ -1,5 +1,5 @@
-// device.h — device-side building blocks shared by the megakernel (render.hip) and
-// the wavefront pipeline (wavefront.hip).  IEEE binary64 throughout; every function
+// device.h — device-side building blocks of the render kernels (render.hip, render_full.h).
+// IEEE binary64 throughout; every function
 // restates a reference routine (file:line cited) in the same operation order.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -203,6 +203,32 @@ struct Stack {
         tlo = __hiloint2double((int)(unsigned)(e >> 32), 0);
         return (int)(unsigned)(e & 0xffffffffull);
     }
+    // raw 64-bit entries (wide.h packs {ref, float entry distance})
+    __device__ __forceinline__ void push_raw_if(bool keep, unsigned long long e) {
+        if (lds_only()) {
+            lds[sp * stride] = e;
+        } else if (sp < kLds) {
+            lds[sp * stride] = e;
+        } else if (keep) {
+            asm volatile("" ::: "memory");
+            spill[sp - kLds] = e;
+        }
+        sp += keep ? 1 : 0;
+    }
+    __device__ __forceinline__ unsigned long long pop_raw() {
+        --sp;
+        unsigned long long e;
+        if (lds_only()) {
+            e = lds[sp * stride];
+        } else {
+            e = lds[min(sp, kLds - 1) * stride];
+            if (sp >= kLds) {
+                asm volatile("" ::: "memory");
+                e = spill[sp - kLds];
+            }
+        }
+        return e;
+    }
     // drop every entry above `base`
     __device__ __forceinline__ void reset(int base) { sp = base; }
 };
@@ -228,6 +254,7 @@ struct Counts {
     // per walk iteration ([0] closest, [1] any-hit): waves whose lanes took an inner step /
     // a leaf run / the scalar-cache inner step, and lanes that took an inner step / a leaf
     unsigned long long it_wave_inner[2], it_wave_leaf[2], it_wave_scalar[2], it_lane_inner[2], it_lane_leaf[2];
+    unsigned ties;                              // wide walks re-walked in reference order (equal-t hits)
 };
 constexpr int kMissRef = 0x7fffffff;   // count_ref any-hit: a pushed child whose slab test missed
 
@@ -446,9 +473,6 @@ __device__ __forceinline__ bool inner_step_rec(const RenderParams& P, const Rec&
 // at the same node.  Vector loads of one node by 64 lanes return 64 copies through the
 // texture-data path (7 instructions x 1 KB per wave step), which profiling showed ~90%
 // busy (TD_TD_BUSY); the scalar path moves the 104 B once, through the scalar cache.
-#ifndef MYRT_SCALAR_FULL
-#define MYRT_SCALAR_FULL 1      // wave-uniform steps on full (FP64) records through SGPRs too (A/B)
-#endif
 #ifndef MYRT_SCALAR_COMPACT
 #define MYRT_SCALAR_COMPACT 1   // wave-uniform steps on compact BLAS records read them (16 SGPRs, not 26)
 #endif
@@ -507,10 +531,8 @@ __device__ __forceinline__ bool inner_step(const RenderParams& P, int& ref, cons
             return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
         }
 #endif
-#if MYRT_SCALAR_FULL
         const SRec R = load_rec_scalar(P.recs + r0);
         return inner_step_rec<COUNT, FAST, SHADOW>(P, R, ref, o, inv, lim, st, c);
-#endif
     }
     if (COUNT && !P.count_ref) {             // redundancy of the per-lane loads below
         unsigned long long left = __ballot(1);
@@ -709,25 +731,7 @@ __device__ __forceinline__ bool unified_leaf(const RenderParams& P, int ref, Sta
             tri_closest(T, o, d, tlo, eps, h, t, T.prim, P.fast_rcp);   // prim = owning instance
             return false;
         };
-#ifndef MYRT_LEAF_PREFETCH
-#define MYRT_LEAF_PREFETCH 0
-#endif
         auto run = [&](const auto* tris) -> bool {
-            if (MYRT_LEAF_PREFETCH) {
-                // both triangles of a pair are loaded before the first test, so the second load's
-                // latency hides behind the first test; tris[t + 1] is always readable (the device
-                // arrays carry one zeroed record past the end, render.hip upload_padded).  The
-                // tests themselves stay in leaf order (strict <, RTContext.swift:573-597).
-                for (int t = e;; t += 2) {
-                    const auto T0 = tris[t];
-                    const auto T1 = tris[t + 1];
-                    if (test(T0, t)) return true;
-                    if (T0.last) break;
-                    if (test(T1, t + 1)) return true;
-                    if (T1.last) break;
-                }
-                return false;
-            }
             for (int t = e;; ++t) {
                 const auto T = tris[t];          // by value: `last` arrives with the vertices
                 if (test(T, t)) return true;
@@ -785,7 +789,16 @@ __device__ __forceinline__ bool unified_begin(const RenderParams& P, const V3& o
     return true;
 }
 
-// Whole-ray unified walks (identity scenes): closest hit and any hit with one stack.
+}  // namespace dev
+}  // namespace myrt
+#include "wide.h"
+namespace myrt {
+namespace dev {
+
+// Whole-ray unified walks (identity scenes): closest hit and any hit with one stack.  With a
+// wide tree (RenderParams::wide) and every 1/d in range, the conservative FP32 four-wide walk
+// (wide.h) runs instead; a lane that met two candidates at its final t is re-walked here in
+// the reference's order.  Counting launches keep the binary walk (reference-order tallies).
 template <bool COUNT, bool FAST>
 __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
                                                  double tlo, Hit& h, Stack& st, Counts& c) {
@@ -799,6 +812,16 @@ template <bool COUNT>
 __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
                                             double tlo, Hit& h, Stack& st, Counts& c) {
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    if (!COUNT && P.wide && __all(wide_ok(inv))) {
+        bool tie = false;
+        (void)wide_walk<false>(P, o, d, inv, tlo, DINF, h, tie, st);
+        if (__any(tie) && tie) {                 // equal-t candidates: the reference's order decides
+            c.ties++;
+            h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+            uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
+        }
+        return;
+    }
     if (__all(finite3(inv))) uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
     else uni_closest_walk<COUNT, false>(P, o, d, inv, tlo, h, st, c);
 }
@@ -822,6 +845,11 @@ __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o,
                                              Stack& st, Counts& c) {
     if (!P.has_tlas) return false;
     const V3 inv = rcp(d);
+    if (!COUNT && P.wide && __all(wide_ok(inv))) {
+        Hit hu;
+        bool tie = false;
+        return wide_walk<true>(P, o, d, inv, 0.0, tmax, hu, tie, st);
+    }
     if (__all(finite3(inv))) return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
     return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);
 }

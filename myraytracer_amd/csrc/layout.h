@@ -60,6 +60,23 @@ struct alignas(16) CTri {
 };
 static_assert(sizeof(CTri) == 48, "CTri is 48 B");
 
+// Four-wide node of the conservative FP32 walk (wide.h), built for identity scenes by collapsing
+// the unified TLAS + BLAS tree (scene.cpp build_wide).  Only the reference's LEAVES matter to
+// the result: with every 1/d finite, child boxes nest inside parent boxes (node bounds are
+// min/max over a subset of the parent's primitives, BVH.swift:108-124, 184-185) and the FP64
+// slab test is monotone in the bounds, so intersectBLAS tests exactly the triangles whose leaf
+// box passes hitAABB.  Inner boxes here are rounded outward to float; the walk widens them
+// further per render (RenderParams::wdelta) so a conservative FP32 test passes whenever the
+// reference's FP64 test of any leaf below passes.  Leaf boxes are then checked exactly (FP64,
+// lbox) before a hit is accepted.  Slots [axis][child], SoA per axis.
+struct alignas(128) W4Node {
+    float lo[3][4];       // child c box min along axis a: lo[a][c] (rounded down)
+    float hi[3][4];       // ... max (rounded up); an empty slot has lo = hi = +inf (never hit)
+    int32_t ref[4];       // >= 0: W4Node index; < 0: ~first TriRec of a reference leaf run
+    int32_t pad[4];
+};
+static_assert(sizeof(W4Node) == 128, "W4Node is one 128-B line");
+
 struct DMaterial {        // ParsingKit Material fields used by trace()
     double ambient[3], diffuse[3], specular[3], mirror[3], absorption[3];
     double phong, ior, absorption_index, roughness;
@@ -156,7 +173,6 @@ struct RenderParams {
     int32_t count_ref;               // COUNT launches: walk + tally in reference order (device.h Counts)
     int32_t xcd_remap;               // megakernel: tiles per XCD run (device.h xcd_tile; <= 1 = identity)
     int32_t compact_limit;           // records below this index are read from crecs
-    int32_t rot_slots;               // megakernel dispatch order: selected chunk rows rotated by this many
     int32_t fast_rcp;                // every Moeller-Trumbore |det| >= eps lies in [2^-700, 2^1000]
                                      // (host bound): 1/det by device.h rcp_rn, bit-identical
     const DAreaLight* alights;
@@ -207,6 +223,17 @@ struct RenderParams {
     int32_t tree_size;
     uint8_t* nflags;
     int32_t tree_ppw;                // node positions per wave in k_level / k_shade
+    // conservative FP32 four-wide walk (wide.h; identity scenes): nodes, the root node, the exact
+    // FP64 box of every reference leaf by its first TriRec (6 doubles), the per-render widening of
+    // every box (wdelta, world units: covers the FP32 rounding of o*inv for every ray origin of
+    // the render) and the FP32 form of eps rounded down.  wide == 0: the binary FP64 walk.
+    const W4Node* wnodes;
+    const double* lbox;
+    int32_t wide;
+    int32_t wide_root;
+    double wdelta;
+    float weps;
+    int32_t wide_pad;
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters
@@ -216,6 +243,7 @@ constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters
 constexpr int kQueueCount = 32, kQueueTiles = 48;
 constexpr int kMaxQueueLevels = 15;
 constexpr int kCounterShadowTraced = 13;
+constexpr int kCounterTies = 26;     // wide walks re-walked in reference order (equal-t candidates, wide.h)
 constexpr int kMaxDepthGPU = 16;     // trace() levels kept in private memory per lane (deeper: RenderParams::deep)
 constexpr int64_t kDeepBytesCap = 8ll << 30;   // device bytes of deep frames per launch batch
 

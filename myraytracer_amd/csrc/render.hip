@@ -29,7 +29,6 @@
 #include "device.h"
 #include "layout.h"
 #include "scene.h"
-#include "wavefront.h"
 
 namespace myrt {
 namespace dev {
@@ -275,7 +274,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 }
 
 
-// One wave renders an 8x8 tile of one 8-row chunk; blocks hold block_threads()/64 waves.
+// One wave renders an 8x8 tile of one 8-row chunk; one wave per block (kRenderBlock).
 #ifndef MYRT_MEGA_WPE
 #define MYRT_MEGA_WPE 4      // amdgpu_waves_per_eu for the megakernel (0 = compiler default = 2 waves at ~200 VGPRs)
 #endif
@@ -283,15 +282,8 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 #define MYRT_PIXLDS 1        // pixel sum + PCG32 state kept in LDS across the walks (not spilled)
 #endif
 constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;
-#ifndef MYRT_TILE_W
-#define MYRT_TILE_W 8        // megakernel tile width in pixels (8: 8x8 tiles; 16: 16x4; 32: 32x2)
-#endif
-constexpr int kTileW = MYRT_TILE_W;
-static_assert(kTileW == 8 || kTileW == 16 || kTileW == 32, "MYRT_TILE_W: 8, 16 or 32");   // x, y, z, rng.state (8 B x 64 lanes each)
+constexpr int kTileW = 8;    // 8x8 pixel tiles (16x4 / 32x2 measured slower: DESIGN.md §4)
 typedef __attribute__((address_space(3))) double lds_f64;
-#ifndef MYRT_BOUNCE_UNI_SPILL
-#define MYRT_BOUNCE_UNI_SPILL 0   // wave-uniform LDS-only stack push/pop in the bounce kernel too
-#endif
 #ifndef MYRT_BOUNCE_WPE
 #define MYRT_BOUNCE_WPE 6   // the bounce (mirror/conductor) instantiation: 6 waves/SIMD (80 VGPRs; C5 -7.5 %)
 #endif
@@ -324,16 +316,11 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     // one tile = (TW x waves-per-block) x TH pixels of one selected chunk (one TW x TH
-    // rectangle per wave, TW = MYRT_TILE_W); tiles are row-major over (slot, band, column)
+    // rectangle per wave, TW = kTileW); tiles are row-major over (slot, band, column)
     constexpr int TW = kTileW, TH = 64 / kTileW, BANDS = 8 / TH;
     const int wpb = (int)(blockDim.x >> 6);
     const int gx = (P.cam.width + TW * wpb - 1) / (TW * wpb);
-    int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
-    // rotated dispatch order: the first rot_slots chunk rows go last (host: MYRT_ROTATE)
-    if (P.rot_slots > 0) {
-        tile += P.rot_slots * gx * BANDS;
-        if (tile >= (int)gridDim.x) tile -= (int)gridDim.x;
-    }
+    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
     const int i = (tile % gx) * (TW * wpb) + wave * TW + (lane % TW);
     const int slot = tile / (gx * BANDS);              // position in the selected chunk list
     const int chunk = P.chunk_first + slot * P.chunk_step;
@@ -348,7 +335,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 #endif
     if (valid) {
         MYRT_STACK(st, lds_stack);
-        st.uni_spill = !BOUNCE || MYRT_BOUNCE_UNI_SPILL;
+        st.uni_spill = !BOUNCE;     // the LDS-only fast path raised the bounce kernel's spills
         PCG32 rng(pixel_seed(i, j));
         V3 pixel = v3(0, 0, 0);
         const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
@@ -448,11 +435,12 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 #endif
     // ray / work counters: one atomic per wave
     const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
-                             s2 = wave_sum(cnt.shadow_traced);
+                             s2 = wave_sum(cnt.shadow_traced), s3 = wave_sum(cnt.ties);
     if (lane == 0) {
         if (s0) atomicAdd(&P.counters[0], s0);
         if (s1) atomicAdd(&P.counters[1], s1);
         if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
+        if (s3) atomicAdd(&P.counters[kCounterTies], s3);
     }
     if (COUNT) {
         const unsigned long long a = wave_sum(cnt.recs), b = wave_sum(cnt.tris), cc = wave_sum(cnt.normals),
@@ -688,11 +676,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
         }
     }
     const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
-                             s2 = wave_sum(cnt.shadow_traced);
+                             s2 = wave_sum(cnt.shadow_traced), s3 = wave_sum(cnt.ties);
     if (lane == 0) {
         if (s0) atomicAdd(&P.counters[0], s0);
         if (s1) atomicAdd(&P.counters[1], s1);
         if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
+        if (s3) atomicAdd(&P.counters[kCounterTies], s3);
     }
 }
 
@@ -769,13 +758,15 @@ static int32_t fail(int32_t code, const std::string& msg) { g_err = msg; return 
         if (_e != hipSuccess) return fail(RT_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
 
-constexpr int kRenderBlock = 64;    // default threads per render block (block_threads): one wave
+// Threads per render block: one wave.  A block's LDS and wave slots are released only when ALL
+// of its waves finish, and wave durations vary ~4x across neighbouring 8x8 tiles: with 4-wave
+// blocks ~25% of the wave slots sat idle behind a block's slowest wave (tools/probe_timeline.py).
+constexpr int kRenderBlock = 64;
 constexpr int kRenderBatches = 8;   // rt_render: chunk batches per replica (progress / overlap granularity)
 // rt_render_submit: renders in flight per scene.  Each has its own stream, counters and events
 // on every replica, so consecutive frames overlap on the GPU: the next frame's tiles fill the
 // compute units the previous frame's slowest tiles leave idle (tools/probe_overlap.py).
 constexpr int kInFlight = RT_MAX_IN_FLIGHT;
-constexpr int kSubmitDmaDefault = 0;   // rt_render_submit delivery (MYRT_SUBMIT_DMA, submit_impl)
 // Queued bounce rays of one stream's renders (BounceRec, levels x records per level)
 struct BounceArena {
     void* base = nullptr;                          // records, tile masks, tile list (queue_arena)
@@ -783,16 +774,13 @@ struct BounceArena {
 };
 // Compacted bounce render: device bytes one launch may take for its queues (else the megakernel)
 constexpr int64_t kQueueBytesCap = 16ll << 30;
-// Off by default: parity-green but slower than the bounce megakernel on C5 (DESIGN.md §4,
-// "Compacted bounce render"); MYRT_QUEUE=1 selects it.
-constexpr int32_t kQueueDefault = 0;
-// rt_render_submit: full trace() renders (render_full.h) overlapping on their own slot streams,
-// each slot with its own pass scratch (C3g: ~7.8 GB per slot); MYRT_FULL_FLIGHTS overrides
-constexpr int32_t kFullFlights = 4;
+// (The compacted bounce render is off by default, option queue: parity-green but slower than the
+// bounce megakernel on C5, DESIGN.md §4 "Compacted bounce render".)
 // Scratch of the full trace() passes (render_full.h), grown on demand: per-pixel area-light
 // event counts and jitter prefixes, the closest-hit log, the node-parallel shading records and
 // the level passes' node flags.  The replica has one (rt_render, in-order renders) and each
-// of the first kFullFlights in-flight slots one (rt_render_submit: overlapping full renders).
+// of the first `full_flights` in-flight slots one (option, default 4; rt_render_submit:
+// overlapping full renders, C3g: ~7.8 GB of scratch per slot).
 struct FullScratch {
     long long* events = nullptr;
     long long* jstart = nullptr;
@@ -834,6 +822,8 @@ struct DeviceReplica {
     CRec* crecs = nullptr;
     CTri* ctris = nullptr;
     TriRec* tris = nullptr;
+    W4Node* wnodes = nullptr;                 // conservative four-wide walk (wide.h)
+    double* lbox = nullptr;
     double* normals = nullptr;
     DInstance* insts = nullptr;
     DTlasLeafEntry* tlas_leaf = nullptr;
@@ -860,14 +850,53 @@ struct DeviceReplica {
     int64_t bytes = 0;
     int cus = 256;                            // compute units (k_bounce grid)
     BounceArena arena;                        // compacted bounce queues of the replica stream
-    WaveBuffers wave;                         // wavefront-pipeline queues (grown on demand)
+    // rt_render_device / rt_render_device_counted (the caller's stream): counters, pass scratch and
+    // queues of their own, so device renders may overlap the replica-stream and slot renders
+    unsigned long long* dev_counters = nullptr;
+    FullScratch dev_full;
+    BounceArena dev_arena;
     Flight fl[kInFlight];                     // rt_render_submit slots
 };
 
 }  // namespace
 
+// ---- render options (rt_scene_set_option, rtcore.h): tuning and test switches whose defaults are
+// the production settings.  They replace the MYRT_* environment switches of earlier rounds: the
+// library reads no environment variable on the render path.
+enum OptId {
+    kOptWide, kOptUnified, kOptUnifiedTransformed, kOptCompactRecords, kOptCompactTris, kOptXcdGroup,
+    kOptQueue, kOptQueueLevels, kOptHitlog, kOptNodeshade, kOptLevels, kOptTreePpw, kOptFullFlights,
+    kOptDeepCapMb, kOptBatches, kOptZerocopy, kOptSubmitEvents, kOptSubmitCounters, kOptSubmitDma,
+    kOptDebugFailReplica, kOptCount
+};
+struct OptDef { const char* name; int64_t def, lo, hi; };
+static const OptDef kOptDefs[kOptCount] = {
+    {"wide", 1, 0, 1},                    // conservative FP32 four-wide walk on identity scenes (wide.h)
+    {"unified", 1, 0, 1},                 // one-stack TLAS+BLAS walks (0: the nested general walk)
+    {"unified_transformed", 1, 0, 1},     // the unified transformed walk for instanced scenes (device.h ut_walk)
+    {"compact_records", 1, 0, 1},         // float32-bound BLAS records when exact (layout.h CRec)
+    {"compact_tris", 1, 0, 1},            // float32-vertex triangles when exact (layout.h CTri)
+    {"xcd_group", 0, 0, 64},              // tiles per XCD run (device.h xcd_tile); 0 = max(2, width / 960)
+    {"queue", 0, 0, 1},                   // compacted bounce render for mirror scenes (k_qscan / k_bounce)
+    {"queue_levels", -1, -1, 15},         // timing probe: bounce levels of the compacted render (-1 = all)
+    {"hitlog", -1, -1, 64},               // closest hits logged per pixel for render_full (-1 = sized automatically)
+    {"nodeshade", 1, 0, 1},               // node-parallel shading of logged hits (render_full.h k_shade)
+    {"levels", 1, 0, 1},                  // breadth-first events passes (render_full.h k_level)
+    {"tree_ppw", 4, 1, 64},               // trace() tree node positions per wave in k_level / k_shade
+    {"full_flights", 4, 0, RT_MAX_IN_FLIGHT},  // full trace() renders overlapping on slot streams
+    {"deep_cap_mb", 8192, 1, 1 << 20},    // device MB of deep trace() frames per launch batch
+    {"batches", 0, 0, 8},                 // rt_render launches per replica (0 = automatic)
+    {"zerocopy", 1, 0, 1},                // kernels store page-locked outputs directly (0: staged copies)
+    {"submit_events", 1, 0, 1},           // kernel-timing events on renders that ask for them
+    {"submit_counters", 1, 0, 1},         // ray counters delivered per submitted render
+    {"submit_dma", 0, 0, 2},              // submitted delivery: 0 kernel stores, 1 staging + DMA, 2 staging only
+    {"debug_fail_replica", -1, -1, 1 << 20},   // test hook: launch failure injected on this replica
+};
+
 struct rt_scene {
     HostScene host;
+    int64_t opt[kOptCount];
+    rt_scene() { for (int k = 0; k < kOptCount; ++k) opt[k] = kOptDefs[k].def; }
     std::vector<DeviceReplica> devs;
     std::mutex mu;
     double upload_ms = 0;
@@ -883,6 +912,21 @@ struct rt_scene {
     int64_t next_ticket = 0;
 };
 
+static int64_t full_scratch_bytes(const FullScratch& f) {
+    return f.cap_px * 16 + f.hitlog_cap * (int64_t)sizeof(DHitRec) +
+           f.nodes_cap * (int64_t)(sizeof(DNodeRec) + 3 * sizeof(double)) + f.walks_cap * 4 + f.nflags_cap;
+}
+static int64_t arena_bytes(const BounceArena& a) {
+    return a.base ? a.levels * a.tiles * 64 * (int64_t)sizeof(BounceRec) + a.levels * a.tiles * 8 + a.tiles * 8 : 0;
+}
+// device scratch a replica holds now (rt_scene_info.scratch_bytes): grown on demand, kept for reuse
+static int64_t scratch_bytes(const DeviceReplica& r) {
+    int64_t b = full_scratch_bytes(r.full) + full_scratch_bytes(r.dev_full) + arena_bytes(r.arena) +
+                arena_bytes(r.dev_arena) + r.deep_cap + r.out_cap_px * 28 + r.wave_times_cap * 24;
+    for (const Flight& f : r.fl) b += full_scratch_bytes(f.full) + arena_bytes(f.arena) + f.stage_px * 28;
+    return b;
+}
+
 template <class T>
 static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
     const size_t n = std::max<size_t>(1, v.size());
@@ -894,13 +938,16 @@ static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
 
 static void free_replica(DeviceReplica& r) {
     (void)hipSetDevice(r.device);
-    wave_release(r.wave);
+    (void)hipFree(r.wnodes); (void)hipFree(r.lbox);
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.wave_times);
     (void)hipFree(r.deep);
     r.full.release();
+    r.dev_full.release();
     (void)hipFree(r.arena.base);
+    (void)hipFree(r.dev_arena.base);
+    (void)hipFree(r.dev_counters);
     if (r.ev0) (void)hipEventDestroy(r.ev0);
     if (r.ev1) (void)hipEventDestroy(r.ev1);
     if (r.counters_ready) (void)hipEventDestroy(r.counters_ready);
@@ -928,8 +975,7 @@ static void free_replica(DeviceReplica& r) {
     r = DeviceReplica();
 }
 
-// Triangle arrays get one zeroed record past the end: a leaf walk may load the record after a
-// run's last triangle before it looks at `last` (device.h MYRT_LEAF_PREFETCH).
+// Triangle arrays get one zeroed record past the end (a guard record after the last run).
 template <class T>
 static int32_t upload_padded(const std::vector<T>& v, T** dst, int64_t& bytes) {
     const size_t n = v.size() + 1;
@@ -964,12 +1010,16 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
         if ((rc = replicate(S.ctris, src->ctris, sd, &r.ctris, device, r.bytes, true)) != RT_OK) return rc;
         if ((rc = replicate(S.tris, src->tris, sd, &r.tris, device, r.bytes, true)) != RT_OK) return rc;
         if ((rc = replicate(S.normals, src->normals, sd, &r.normals, device, r.bytes)) != RT_OK) return rc;
+        if ((rc = replicate(S.wnodes, src->wnodes, sd, &r.wnodes, device, r.bytes)) != RT_OK) return rc;
+        if ((rc = replicate(S.lbox, src->lbox, sd, &r.lbox, device, r.bytes)) != RT_OK) return rc;
     } else {
         if ((rc = upload(S.recs, &r.recs, r.bytes)) != RT_OK) return rc;
         if ((rc = upload(S.crecs, &r.crecs, r.bytes)) != RT_OK) return rc;
         if ((rc = upload_padded(S.ctris, &r.ctris, r.bytes)) != RT_OK) return rc;
         if ((rc = upload_padded(S.tris, &r.tris, r.bytes)) != RT_OK) return rc;
         if ((rc = upload(S.normals, &r.normals, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload(S.wnodes, &r.wnodes, r.bytes)) != RT_OK) return rc;
+        if ((rc = upload(S.lbox, &r.lbox, r.bytes)) != RT_OK) return rc;
     }
     if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.tlas_leaf, &r.tlas_leaf, r.bytes)) != RT_OK) return rc;
@@ -979,6 +1029,8 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
     if ((rc = upload(S.jitter, &r.jitter, r.bytes)) != RT_OK) return rc;
     HIP_TRY(hipMalloc((void**)&r.counters, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(r.counters, 0, kCounterWords * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&r.dev_counters, kCounterWords * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(r.dev_counters, 0, kCounterWords * sizeof(unsigned long long)));
     if (hipDeviceGetAttribute(&r.cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || r.cus <= 0) {
         (void)hipGetLastError();
         r.cus = 256;
@@ -1059,23 +1111,20 @@ static DCamera camera_constants(const rt_camera& cam) {
     return C;
 }
 
-static int block_threads();
-// Device bytes of deep frames per launch batch (MYRT_DEEP_CAP_MB overrides, for tests)
-static double deep_cap() {
-    const char* e = std::getenv("MYRT_DEEP_CAP_MB");
-    return (e && *e) ? std::max(1.0, std::atof(e)) * 1048576.0 : (double)kDeepBytesCap;
-}
+// Device bytes of deep frames per launch batch (option deep_cap_mb; default kDeepBytesCap)
+static double deep_cap(const rt_scene* s) { return (double)s->opt[kOptDeepCapMb] * 1048576.0; }
 // Lanes of one selected 8-row chunk (render_grid) times the deep trace() levels per lane.
 static double deep_bytes_per_chunk(int32_t max_depth, int32_t width) {
-    const int bt = block_threads(), px = 8 * (bt / 64);
+    const int bt = kRenderBlock, px = 8 * (bt / 64);
     const double lanes = (double)((std::max(1, width) + px - 1) / px) * bt;
     return lanes * (double)std::max(0, max_depth - kMaxDepthGPU) * (double)sizeof(dev::Frame);
 }
-static int32_t check_renderable(const HostScene& S, int32_t cam) {
+static int32_t check_renderable(const rt_scene* s, int32_t cam) {
+    const HostScene& S = s->host;
     if (cam < 0 || cam >= (int32_t)S.cams.size()) return fail(RT_ERR_INVALID_CAMERA, "Invalid camera index");
     // trace() levels beyond kMaxDepthGPU live in a device buffer, one Frame per level and lane
     // of a launch batch (render_full<.., DEEP>); one 8-row chunk's lanes must fit kDeepBytesCap
-    if (S.max_depth > kMaxDepthGPU && deep_bytes_per_chunk(S.max_depth, S.cams[cam].width) > deep_cap())
+    if (S.max_depth > kMaxDepthGPU && deep_bytes_per_chunk(S.max_depth, S.cams[cam].width) > deep_cap(s))
         return fail(RT_ERR_UNSUPPORTED, "maxRecursionDepth too deep for the device frame buffer");
     return RT_OK;
 }
@@ -1090,11 +1139,6 @@ extern "C" int32_t rt_rows_for_chunks(int32_t height, int32_t chunk_first, int32
     return rows;
 }
 
-static int32_t env_int(const char* name, int32_t def, int32_t lo, int32_t hi) {
-    const char* v = std::getenv(name);
-    if (!v || !*v) return def;
-    return std::min(hi, std::max(lo, (int32_t)std::atoi(v)));
-}
 
 // Absolute pruning margin for rays whose origins lie within `origin_dist` of the scene
 // center (or inside the scene bounds): prune_k * (|o - v0| + t|d|) with both terms bounded
@@ -1119,6 +1163,21 @@ static double dist_to_center(const HostScene& S, const double p[3]) {
     return std::sqrt(d);
 }
 
+// The conservative four-wide walk (wide.h) for this render: every ray origin has coordinates of
+// magnitude <= origin_coord (camera + lens) or lies inside the scene bounds (hit points, offset by
+// shadowRayEpsilon).  wdelta = 8 * 2^-24 * max(|box coordinate|, |origin coordinate|) bounds the
+// FP32 rounding of the slab terms (wide.h header); weps = eps rounded down to float.
+static void set_wide(const HostScene& S, const DeviceReplica& r, RenderParams& P, double origin_coord, bool on) {
+    P.wnodes = r.wnodes; P.lbox = r.lbox; P.wide_root = S.wide_root;
+    const double R = std::max(S.wide_coord, origin_coord) + std::fabs(S.shadow_eps) + std::fabs(S.eps);
+    P.wdelta = R * 0x1p-21;
+    float we = (float)S.eps;
+    if ((double)we > S.eps) we = std::nextafter(we, -HUGE_VALF);
+    P.weps = we;
+    P.wide = (S.wide_root >= 0 && r.wnodes && R < 0x1p27 && R > 0x1p-60 && std::isfinite(R) &&
+              on) ? 1 : 0;
+}
+
 static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32_t cam, int32_t first, int32_t step,
                                 double* out_rgb, uint8_t* out_rgba8) {
     const HostScene& S = s->host;
@@ -1131,7 +1190,7 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.tlas_leaf_base = (int32_t)S.tlas_leaf_base;
     P.identity = S.identity ? 1 : 0;
     // one stack for TLAS + BLAS + a TLAS leaf's markers (HostScene::max_stack_unified)
-    P.ut = (S.has_tlas && S.max_stack_unified <= kStackCap && env_int("MYRT_UT", 1, 0, 1) == 1) ? 1 : 0;
+    P.ut = (S.has_tlas && S.max_stack_unified <= kStackCap && s->opt[kOptUnifiedTransformed] != 0) ? 1 : 0;
     P.tlas_rec_base = (int32_t)S.blas_records;
     P.ut_marker_base = (int32_t)(S.tlas_leaf_base + (int64_t)S.tlas_leaf.size());
     P.num_mats = (int32_t)S.mats.size();
@@ -1158,16 +1217,12 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.num_chunks = nsel;
     P.stack_depth = dev::kLds;
     {
-        const char* xe = std::getenv("MYRT_XCD");                // tile-group size per XCD (device.h xcd_tile)
-        // runs of G neighbouring 8x8 tiles per XCD; measured best: G = 2 at 1920 px (C3),
-        // G = 4 at 3840 px (C5), i.e. about one run per 960 px of image width
-        P.xcd_remap = xe ? std::atoi(xe) : std::max(2, P.cam.width / 960);
-        const char* oe = std::getenv("MYRT_ROTATE");             // dispatch order: chunk rows rotated
-        P.rot_slots = oe ? std::max(0, std::min(std::atoi(oe), nsel - 1)) : 0;
-        const char* ce = std::getenv("MYRT_COMPACT");           // A/B switch: MYRT_COMPACT=0
-        P.compact_limit = (ce && ce[0] == '0') ? 0 : (int32_t)S.compact_records;
-        const char* te = std::getenv("MYRT_CTRI");              // A/B switch: MYRT_CTRI=0
-        P.ctris = (S.compact_tris && !(te && te[0] == '0')) ? r.ctris : nullptr;
+        // runs of G neighbouring 8x8 tiles per XCD (device.h xcd_tile); measured best: G = 2 at
+        // 1920 px (C3), G = 4 at 3840 px (C5), i.e. about one run per 960 px of image width
+        const int64_t xg = s->opt[kOptXcdGroup];
+        P.xcd_remap = xg > 0 ? (int32_t)xg : std::max(2, P.cam.width / 960);
+        P.compact_limit = s->opt[kOptCompactRecords] ? (int32_t)S.compact_records : 0;
+        P.ctris = (S.compact_tris && s->opt[kOptCompactTris]) ? r.ctris : nullptr;
     }
     P.out_rgb = out_rgb; P.out_rgba8 = out_rgba8;
     P.counters = r.counters;
@@ -1176,6 +1231,12 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
     P.jitter = r.jitter;
     P.num_alights = (int32_t)S.alights.size();
     P.has_special = S.has_special ? 1 : 0;
+    {
+        const rt_camera& cam0 = S.cams[cam];
+        const double ce[3] = {cam0.position.x, cam0.position.y, cam0.position.z};
+        set_wide(S, r, P, std::max({std::fabs(ce[0]), std::fabs(ce[1]), std::fabs(ce[2])}) + std::fabs(cam0.aperture_size),
+                 s->opt[kOptWide] != 0);
+    }
     return P;
 }
 
@@ -1188,33 +1249,14 @@ static bool scene_is_rough(const HostScene& S) {
     }
     return false;
 }
-// breadth-first events passes for area-light frames (render_full.h k_level; MYRT_LEVELS)
-constexpr int32_t kLevelsDefault = 1;
-// node positions of a tree level one wave of k_level / k_shade runs (MYRT_TREE_PPW): one per wave
-// dispatches mostly empty waves at the deep levels, all in one wave makes a tile's positions a
-// serial chain (the slowest tile bounds a pass)
-constexpr int32_t kTreePpwDefault = 4;
+// (Option tree_ppw, the node positions of a tree level one wave of k_level / k_shade runs: one
+// per wave dispatches mostly empty waves at the deep levels, all in one wave makes a tile's
+// positions a serial chain, the slowest tile bounding a pass; 4 is measured best.)
 static bool scene_has_bounce(const HostScene& S) {
     for (const auto& m : S.mats) if (m.type == RT_MAT_MIRROR || m.type == RT_MAT_CONDUCTOR) return true;
     return false;
 }
 
-// MYRT_PATH=wave selects the wavefront pipeline (wavefront.hip); default: the
-// single-kernel path, currently the faster one on C3 (profiles/r01_*).
-static bool use_megakernel() {
-    const char* e = std::getenv("MYRT_PATH");   // read per launch so tests can A/B in one process
-    return !(e && std::strcmp(e, "wave") == 0);
-}
-
-// Threads per render block.  A block's LDS and wave slots are released only when ALL of
-// its waves finish, and wave durations vary ~4x across neighbouring 8x8 tiles: with 4-wave
-// blocks ~25% of the wave slots sat idle behind a block's slowest wave
-// (tools/probe_timeline.py).  One-wave blocks free each slot as soon as its wave ends.
-static int block_threads() {
-    const char* e = std::getenv("MYRT_BLOCK");
-    const int v = e ? std::atoi(e) : kRenderBlock;
-    return (v == 64 || v == 128 || v == 256) ? v : kRenderBlock;
-}
 // blocks of `threads` lanes over the selected chunks, one tw x (64/tw) tile per wave
 static dim3 render_grid(const RenderParams& P, int threads, int tw = 8) {
     const int px = tw * (threads / 64);                  // pixels per block along a row
@@ -1233,9 +1275,9 @@ static int64_t hit_slots_for(const RenderParams& P, bool dielectric, int64_t px)
     const int64_t by_mem = kHitLogBytes / std::max<int64_t>(1, px * (int64_t)(sizeof(DHitRec) + sizeof(DNodeRec) + 24));
     return std::max<int64_t>(0, std::min<int64_t>({per_sample * traced, 64, by_mem}));
 }
-static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hipStream_t stream, bool count, bool dielectric,
-                           bool rough) {
-    const int bt = block_threads();
+static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs, RenderParams P, hipStream_t stream,
+                           bool count, bool dielectric, bool rough) {
+    const int bt = kRenderBlock;
     dim3 block((unsigned)bt, 1, 1);
     const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long);
     const unsigned per_slot = render_grid(P, bt).x / (unsigned)std::max(1, P.num_chunks);   // blocks per chunk
@@ -1244,7 +1286,7 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
     int32_t batch = P.num_chunks;
     if (deep) {
         const double per_chunk = deep_bytes_per_chunk(P.max_depth, P.cam.width);
-        batch = (int32_t)std::max(1.0, std::min((double)P.num_chunks, std::floor(deep_cap() / per_chunk)));
+        batch = (int32_t)std::max(1.0, std::min((double)P.num_chunks, std::floor(deep_cap(s) / per_chunk)));
         const int64_t need = (int64_t)(per_chunk * batch);
         if (need > r.deep_cap) {
             (void)hipFree(r.deep);
@@ -1254,8 +1296,7 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
         }
         P.deep = r.deep;
     }
-    const char* ue = std::getenv("MYRT_UNIFIED");
-    const bool unified = P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
+    const bool unified = P.has_tlas && !P.count_ref && s->opt[kOptUnified] != 0;
     const int walk = (unified && P.identity) ? dev::kWalkIdentity
                      : (unified && P.ut && !count) ? dev::kWalkTransformed : dev::kWalkGeneral;
 #define MYRT_BY_WALK(M_)                                                    \
@@ -1286,9 +1327,9 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
         P.events = fs.events;
         P.jstart = fs.jstart;
         // the closest-hit log: render_full reads the first `slots` walks of every pixel back
-        // instead of walking them again (MYRT_HITLOG=K overrides, 0 = off; counting launches walk)
-        const int64_t slots =
-            count ? 0 : env_int("MYRT_HITLOG", (int32_t)hit_slots_for(P, dielectric, px), 0, 64);
+        // instead of walking them again (option hitlog = K overrides, 0 = off; counting launches walk)
+        const int64_t hl = s->opt[kOptHitlog];
+        const int64_t slots = count ? 0 : (hl >= 0 ? hl : hit_slots_for(P, dielectric, px));
         if (slots > 0 && slots * px > fs.hitlog_cap) {
             (void)hipFree(fs.hitlog);
             fs.hitlog = nullptr; fs.hitlog_cap = 0;
@@ -1299,10 +1340,10 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
         P.hits = log ? fs.hitlog : nullptr;
         P.hit_slots = log ? (int32_t)slots : 0;
         P.hit_stride = px;
-        // node-parallel shading of the logged hits (render_full.h k_shade; MYRT_NODESHADE=0: render_full
+        // node-parallel shading of the logged hits (render_full.h k_shade; option nodeshade = 0: render_full
         // shades them).  Every pointer a pass writes through is set here, before the first launch:
         // kernels take RenderParams by value.
-        bool nodeshade = log && env_int("MYRT_NODESHADE", 1, 0, 1) == 1;
+        bool nodeshade = log && s->opt[kOptNodeshade] != 0;
         if (nodeshade && (slots * px > fs.nodes_cap || px > fs.walks_cap)) {
             const int64_t recs = std::max(slots * px, fs.nodes_cap), pxs = std::max(px, fs.walks_cap);
             (void)hipFree(fs.nodes); (void)hipFree(fs.node_lo); (void)hipFree(fs.walks);
@@ -1322,13 +1363,13 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
         P.walks = nodeshade ? fs.walks : nullptr;
         // Breadth-first events passes (render_full.h k_level) when the log holds every pixel's
         // whole trace() trees and no material is rough (no PCG32 draw inside trace(), so the
-        // order of the walks is free); MYRT_LEVELS=0 keeps the depth-first k_events.
+        // order of the walks is free); option levels = 0 keeps the depth-first k_events.
         const int32_t tree = dielectric ? 2 : 1;
         const int64_t traced = std::max(1, std::min(P.cam.samples, P.cam.n * P.cam.n));
         const int64_t tree_size = P.max_depth >= 0 && P.max_depth <= 5
                                       ? (tree == 2 ? (int64_t(2) << P.max_depth) - 1 : P.max_depth + 1) : 0;
         bool levels = nodeshade && !deep && P.has_tlas && tree_size > 0 && slots == tree_size * traced &&
-                      !rough && env_int("MYRT_LEVELS", kLevelsDefault, 0, 1) == 1;
+                      !rough && s->opt[kOptLevels] != 0;
         if (levels && slots * px > fs.nflags_cap) {
             (void)hipFree(fs.nflags);
             fs.nflags = nullptr; fs.nflags_cap = 0;
@@ -1342,7 +1383,7 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
             nodeshade = false;
         }
         P.hit_tree = levels ? tree : 0;
-        P.tree_ppw = env_int("MYRT_TREE_PPW", kTreePpwDefault, 1, 64);
+        P.tree_ppw = (int32_t)s->opt[kOptTreePpw];
         P.tree_size = levels ? (int32_t)tree_size : 0;
         P.nflags = levels ? fs.nflags : nullptr;
         if (levels) {
@@ -1409,8 +1450,8 @@ static int32_t launch_full(DeviceReplica& r, FullScratch& fs, RenderParams P, hi
 // pixels trace one sample (Int(sqrt(spp)) == 1) with maxRecursionDepth <= kMaxQueueLevels;
 // `arena` grows to levels x (tiles x 64) records, the tile masks and k_qscan's tile list
 // (false: allocation refused or failed -> the bounce megakernel).
-static bool queue_arena(BounceArena* arena, RenderParams& P, int64_t tiles) {
-    if (!arena || env_int("MYRT_QUEUE", kQueueDefault, 0, 1) == 0) return false;
+static bool queue_arena(const rt_scene* s, BounceArena* arena, RenderParams& P, int64_t tiles) {
+    if (!arena || s->opt[kOptQueue] == 0) return false;
     if (P.cam.n != 1 || P.max_depth < 1 || P.max_depth > kMaxQueueLevels) return false;
     const int64_t levels = P.max_depth;
     // sections at offsets fixed by the allocation's capacity: the tile masks stay where the
@@ -1453,16 +1494,9 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     // dielectrics, area lights and maxRecursionDepth > kMaxDepthGPU: the full trace()
     // (render_full.h); it and spheres/planes exist only as megakernels
     const bool full = s->host.has_dielectric || P.num_alights > 0 || P.max_depth > kMaxDepthGPU;
-    if (full) return launch_full(r, full_scratch ? *full_scratch : r.full, P, stream, count, s->host.has_dielectric,
+    if (full) return launch_full(s, r, full_scratch ? *full_scratch : r.full, P, stream, count, s->host.has_dielectric,
                                  scene_is_rough(s->host));
-    if (!use_megakernel() && !P.count_ref && !P.has_special) {   // ref-order counting is a megakernel mode
-        const bool bounce_w = scene_has_bounce(s->host) && P.max_depth > 0;
-        const int32_t rc = wave_render(P, r.wave, bounce_w, count, stream);
-        if (rc != RT_OK) return fail(rc, rc == RT_ERR_OOM ? "device allocation of wavefront queues failed"
-                                                         : "wavefront launch failed");
-        return RT_OK;
-    }
-    const int bt = block_threads();
+    const int bt = kRenderBlock;
     dim3 grid = render_grid(P, bt, dev::kTileW);
     dim3 block((unsigned)bt, 1, 1);
     const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long) + (size_t)dev::kPixSlots * bt * sizeof(double);
@@ -1470,8 +1504,7 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     // The walk: identity scenes walk TLAS + BLAS as one tree; other scenes the unified transformed
     // walk (per-instance ray switches), or the nested general walk when the stack bound does not
     // allow one stack or for counting launches (reference-order counting needs the general walk)
-    const char* ue = std::getenv("MYRT_UNIFIED");
-    const bool unified = P.has_tlas && !P.count_ref && !(ue && ue[0] == '0');
+    const bool unified = P.has_tlas && !P.count_ref && s->opt[kOptUnified] != 0;
     const int walk = (unified && P.identity) ? dev::kWalkIdentity
                      : (unified && P.ut && !count) ? dev::kWalkTransformed : dev::kWalkGeneral;
 #define MYRT_LAUNCH(C_, B_, W_) hipLaunchKernelGGL((dev::render_kernel<C_, B_, W_>), grid, block, lds, stream, P)
@@ -1481,7 +1514,7 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
         else M_(dev::kWalkGeneral);                                         \
     } while (0)
-    if (bounce && !count && queue_arena(arena, P, (int64_t)grid.x * (bt / 64))) {
+    if (bounce && !count && queue_arena(s, arena, P, (int64_t)grid.x * (bt / 64))) {
         // primary + shadow rays of every pixel in the spill-free primary instantiation, then per
         // level the tile list (k_qscan) and the level's rays in coherent batches (k_bounce)
 #define MYRT_QPRIM(W_) hipLaunchKernelGGL((dev::render_kernel<false, false, W_, true>), grid, block, lds, stream, P)
@@ -1490,8 +1523,9 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         const dim3 qgrid((unsigned)(r.cus * 4 * MYRT_QUEUE_WPE)), qblock(64);
         const size_t qlds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
         const dim3 sgrid((unsigned)((P.bounce_tiles + dev::kQScanTiles - 1) / dev::kQScanTiles));
-        // MYRT_QUEUE_LEVELS (timing probe only: frames are incomplete below max_depth)
-        const int32_t levels = env_int("MYRT_QUEUE_LEVELS", P.max_depth, 0, P.max_depth);
+        // option queue_levels (timing probe only: frames are incomplete below max_depth)
+        const int64_t ql = s->opt[kOptQueueLevels];
+        const int32_t levels = ql >= 0 ? (int32_t)std::min<int64_t>(ql, P.max_depth) : P.max_depth;
         for (int32_t level = 1; level <= levels; ++level) {
             hipLaunchKernelGGL(dev::k_qcount, sgrid, dim3(dev::kQScanThreads), 0, stream, P, level);
             hipLaunchKernelGGL(dev::k_qscan, sgrid, dim3(dev::kQScanThreads), 0, stream, P, level);
@@ -1568,6 +1602,8 @@ int32_t rt_scene_create(const rt_scene_desc* desc, const int32_t* devices, int32
         s->host.ctris.clear(); s->host.ctris.shrink_to_fit();
         s->host.tris.clear(); s->host.tris.shrink_to_fit();
         s->host.normals.clear(); s->host.normals.shrink_to_fit();
+        s->host.wnodes.clear(); s->host.wnodes.shrink_to_fit();
+        s->host.lbox.clear(); s->host.lbox.shrink_to_fit();
         *out = s;
         return RT_OK;
     } catch (const std::bad_alloc&) {
@@ -1592,7 +1628,31 @@ int32_t rt_scene_info_get(const rt_scene* s, rt_scene_info* out) {
     out->blas_nodes = S.blas_records; out->tlas_nodes = S.tlas_records; out->max_depth = S.max_stack;
     out->build_ms = S.build_ms; out->upload_ms = s->upload_ms;
     out->device_bytes = s->devs.empty() ? 0 : s->devs[0].bytes;
+    out->scratch_bytes = s->devs.empty() ? 0 : scratch_bytes(s->devs[0]);
     return RT_OK;
+}
+
+int32_t rt_scene_set_option(rt_scene* s, const char* name, int64_t value) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
+    if (!name) return fail(RT_ERR_INVALID_ARG, "option name is NULL");
+    for (int k = 0; k < kOptCount; ++k) {
+        if (std::strcmp(name, kOptDefs[k].name) != 0) continue;
+        if (value < kOptDefs[k].lo || value > kOptDefs[k].hi)
+            return fail(RT_ERR_INVALID_ARG, std::string("option ") + name + " out of range [" +
+                                                std::to_string(kOptDefs[k].lo) + ", " + std::to_string(kOptDefs[k].hi) + "]");
+        std::lock_guard<std::mutex> lock(s->mu);
+        s->opt[k] = value;
+        return RT_OK;
+    }
+    return fail(RT_ERR_INVALID_ARG, std::string("unknown option ") + name);
+}
+
+int32_t rt_scene_get_option(const rt_scene* s, const char* name, int64_t* value) {
+    if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
+    if (!name || !value) return fail(RT_ERR_INVALID_ARG, "NULL argument");
+    for (int k = 0; k < kOptCount; ++k)
+        if (std::strcmp(name, kOptDefs[k].name) == 0) { *value = s->opt[k]; return RT_OK; }
+    return fail(RT_ERR_INVALID_ARG, std::string("unknown option ") + name);
 }
 
 int32_t rt_render_device(rt_scene* s, int32_t slot, int32_t cam, int32_t first, int32_t step, double* d_rgb,
@@ -1600,15 +1660,15 @@ int32_t rt_render_device(rt_scene* s, int32_t slot, int32_t cam, int32_t first, 
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
     if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
     if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
-    int32_t rc = check_renderable(s->host, cam);
+    int32_t rc = check_renderable(s, cam);
     if (rc != RT_OK) return rc;
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
-    HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
-    r.counters_zero = false;
+    HIP_TRY(hipMemsetAsync(r.dev_counters, 0, kCounterWords * sizeof(unsigned long long), st));
     RenderParams P = make_params(s, r, cam, first, step, d_rgb, d_rgba8);
-    return launch(s, r, P, st, false, &r.arena);
+    P.counters = r.dev_counters;
+    return launch(s, r, P, st, false, &r.dev_arena, &r.dev_full);
 }
 
 int32_t rt_stats_collect(rt_scene* s, int32_t slot, rt_stats* stats) {
@@ -1617,10 +1677,11 @@ int32_t rt_stats_collect(rt_scene* s, int32_t slot, rt_stats* stats) {
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     unsigned long long c[kCounterWords];
-    HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c, r.dev_counters, sizeof(c), hipMemcpyDeviceToHost));
     if (stats) {
         stats->shadow_rays = (int64_t)c[0]; stats->secondary_rays = (int64_t)c[1];
         stats->shadow_rays_traced = (int64_t)c[kCounterShadowTraced];
+        stats->rewalked = (int64_t)c[kCounterTies];
     }
     return RT_OK;
 }
@@ -1629,27 +1690,26 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
                                  void* stream, rt_work_counters* out) {
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
     if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
-    int32_t rc = check_renderable(s->host, cam);
+    int32_t rc = check_renderable(s, cam);
     if (rc != RT_OK) return rc;
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
-    HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
-    r.counters_zero = false;
+    HIP_TRY(hipMemsetAsync(r.dev_counters, 0, kCounterWords * sizeof(unsigned long long), st));
     RenderParams P = make_params(s, r, cam, first, step, d_rgb, nullptr);
-    rc = launch(s, r, P, st, true);                  // 1) work this path executes
+    P.counters = r.dev_counters;
+    rc = launch(s, r, P, st, true, &r.dev_arena, &r.dev_full);   // 1) work this path executes
     if (rc != RT_OK) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     unsigned long long c[kCounterWords];
-    HIP_TRY(hipMemcpy(c, r.counters, sizeof(c), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemsetAsync(r.counters, 0, kCounterWords * sizeof(unsigned long long), st));
-    r.counters_zero = false;
+    HIP_TRY(hipMemcpy(c, r.dev_counters, sizeof(c), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemsetAsync(r.dev_counters, 0, kCounterWords * sizeof(unsigned long long), st));
     P.count_ref = 1;                                 // 2) the reference's work
-    rc = launch(s, r, P, st, true);
+    rc = launch(s, r, P, st, true, &r.dev_arena, &r.dev_full);
     if (rc != RT_OK) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     unsigned long long q[kCounterWords];
-    HIP_TRY(hipMemcpy(q, r.counters, sizeof(q), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(q, r.dev_counters, sizeof(q), hipMemcpyDeviceToHost));
     if (out) {
         out->records_fetched = (int64_t)c[2]; out->tri_tests = (int64_t)c[3]; out->normal_fetches = (int64_t)c[4];
         out->instance_entries = (int64_t)c[5]; out->pixels = (int64_t)c[6];
@@ -1690,9 +1750,7 @@ int32_t rt_host_alloc(uint64_t bytes, void** out) {
     if (!out) return fail(RT_ERR_INVALID_ARG, "null output pointer");
     *out = nullptr;
     if (bytes == 0) return RT_OK;
-    // MYRT_HOST_NONCOHERENT=1 (A/B switch): coarse-grained pinned memory
-    const unsigned fl = hipHostMallocMapped | hipHostMallocPortable |
-                        (env_int("MYRT_HOST_NONCOHERENT", 0, 0, 1) ? hipHostMallocNonCoherent : 0u);
+    const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
     if (hipHostMalloc(out, bytes, fl) != hipSuccess) {
         (void)hipGetLastError();
         *out = nullptr;
@@ -1731,7 +1789,7 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
     *not_pinned = false;
     // kernel timing events only when asked for (rt_render_ex always asks): each is a packet
     // on the stream, ~1 us of a C4/8 share's 85 us per frame (tools/probe_shares.py)
-    const bool timing = (flags & RT_RENDER_KERNEL_TIME) != 0 && env_int("MYRT_SUBMIT_EVENTS", 1, 0, 1) == 1;
+    const bool timing = (flags & RT_RENDER_KERNEL_TIME) != 0 && s->opt[kOptSubmitEvents] != 0;
     const rt_camera& C = s->host.cams[cam];
     const int32_t W = std::max(1, C.width), H = std::max(1, C.height);
     const bool frame = (flags & RT_RENDER_FRAME_LAYOUT) != 0;
@@ -1746,13 +1804,12 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         return fail(RT_ERR_BUSY, "too many renders in flight: wait for ticket " + std::to_string(fp.ticket) + " first");
     const int32_t D = (int32_t)s->devs.size();
     // Full trace() renders (dielectrics, area lights: render_full) take the stream and pass
-    // scratch of slot q % kFullFlights, so up to kFullFlights of them overlap; deep recursion (one
-    // deep-frame buffer per replica) and the wavefront pipeline (per-replica queues) stay on the
-    // replica's own stream, in order.
+    // scratch of slot q % full_flights, so up to full_flights of them overlap; deep recursion (one
+    // deep-frame buffer per replica) stay on the replica's own stream, in order.
     const bool full = s->host.has_dielectric || !s->host.alights.empty() || s->host.max_depth > kMaxDepthGPU;
-    const int32_t full_flights = env_int("MYRT_FULL_FLIGHTS", kFullFlights, 0, kInFlight);
+    const int32_t full_flights = (int32_t)s->opt[kOptFullFlights];
     const bool full_slots = full && s->host.max_depth <= kMaxDepthGPU && full_flights > 0;
-    const bool concurrent = full ? full_slots : use_megakernel();
+    const bool concurrent = full ? full_slots : true;
     const int qs = full_slots ? q % full_flights : q;  // the slot whose stream (and full scratch) it takes
     const auto t0 = std::chrono::steady_clock::now();
     // the caller's buffers mapped for every replica BEFORE anything is launched: a replica
@@ -1772,16 +1829,16 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
     for (int32_t k = 0; k < D; ++k) s->devs[k].fl[q].used = false;
     // delivery: 0 = the kernel stores the rows into the host buffer; 1 = rows rendered into
     // device staging and copied by the DMA engine; 2 = staging only, not delivered
-    // (measurement switch MYRT_SUBMIT_DMA)
-    const int dma = env_int("MYRT_SUBMIT_DMA", kSubmitDmaDefault, 0, 2);
-    const bool counters_out = env_int("MYRT_SUBMIT_COUNTERS", 1, 0, 1) == 1;
-    const int32_t fail_at = env_int("MYRT_DEBUG_FAIL_REPLICA", -1, -1, 1 << 20);   // test hook
+    // (measurement option submit_dma)
+    const int dma = (int)s->opt[kOptSubmitDma];
+    const bool counters_out = s->opt[kOptSubmitCounters] != 0;
+    const int64_t fail_at = s->opt[kOptDebugFailReplica];   // test hook
     auto launch_one = [&](int32_t k) -> int32_t {
         DeviceReplica& r = s->devs[k];
         Flight& f = r.fl[q];
         const int32_t myFirst = first + k * step, myStep = step * D;
         HIP_TRY(hipSetDevice(r.device));
-        if (k == fail_at) return fail(RT_ERR_DEVICE, "injected launch failure (MYRT_DEBUG_FAIL_REPLICA)");
+        if (k == fail_at) return fail(RT_ERR_DEVICE, "injected launch failure (option debug_fail_replica)");
         hipStream_t st = concurrent ? r.fl[qs].stream : r.stream;
         int32_t nq = 0;
         for (int32_t c = myFirst; c < num_chunks_total(H); c += myStep) nq++;
@@ -1895,13 +1952,15 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
     fp.pending = false;
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("render failed: ") + hipGetErrorString(e));
     double km = 0;
-    int64_t sh = 0, se = 0, stc = 0;
+    int64_t sh = 0, se = 0, stc = 0, rw = 0;
     for (auto& r : s->devs) {
         Flight& f = r.fl[q];
         if (!f.used) continue;
-        // with MYRT_SUBMIT_COUNTERS=0 no counts came back: shadow/secondary stats are reported as 0
+        // with option submit_counters = 0 no counts came back: shadow/secondary stats are reported as 0
         const unsigned long long* c = f.host_counters;
-        if (f.counters_valid) { sh += (int64_t)c[0]; se += (int64_t)c[1]; stc += (int64_t)c[kCounterShadowTraced]; }
+        if (f.counters_valid) {
+            sh += (int64_t)c[0]; se += (int64_t)c[1]; stc += (int64_t)c[kCounterShadowTraced]; rw += (int64_t)c[kCounterTies];
+        }
         float ms = 0;
         if (f.timed && hipEventElapsedTime(&ms, f.ev0, f.ev1) != hipSuccess) (void)hipGetLastError();
         km = std::max(km, (double)ms);
@@ -1912,6 +1971,7 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
         stats->primary_rays = fp.primary;
         stats->shadow_rays = sh; stats->secondary_rays = se; stats->kernel_ms = km;
         stats->shadow_rays_traced = stc;
+        stats->rewalked = rw;
         stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fp.t0).count();
     }
     return RT_OK;
@@ -1925,7 +1985,7 @@ int32_t rt_render_submit(rt_scene* s, int32_t cam, int32_t first, int32_t step, 
     if (flags & ~(uint32_t)(RT_RENDER_FRAME_LAYOUT | RT_RENDER_KERNEL_TIME))
         return fail(RT_ERR_INVALID_ARG, "unknown render flags");
     if (!ticket) return fail(RT_ERR_INVALID_ARG, "ticket is NULL");
-    int32_t rc = check_renderable(s->host, cam);
+    int32_t rc = check_renderable(s, cam);
     if (rc != RT_OK) return rc;
     std::lock_guard<std::mutex> lock(s->mu);
     bool not_pinned = false;
@@ -1955,10 +2015,10 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
     if (s->devs.empty()) return fail(RT_ERR_NO_RENDERER, "Renderer not initialized.");
     if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
     if (flags & ~(uint32_t)RT_RENDER_FRAME_LAYOUT) return fail(RT_ERR_INVALID_ARG, "unknown render flags");
-    int32_t rc = check_renderable(s->host, cam);
+    int32_t rc = check_renderable(s, cam);
     if (rc != RT_OK) return rc;
     std::unique_lock<std::mutex> lock(s->mu);
-    if (!progress && env_int("MYRT_ZEROCOPY", 1, 0, 1) == 1) {
+    if (!progress && s->opt[kOptZerocopy] != 0) {
         // page-locked outputs: one submitted render (the kernels store the rows themselves)
         int64_t t = -1;
         bool not_pinned = false;
@@ -1987,7 +2047,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
     // replicas: each maps the buffer and writes its own chunks' rows
     std::vector<double*> zc_rgb(D, nullptr);
     std::vector<uint8_t*> zc_rgba(D, nullptr);
-    bool zerocopy = direct && env_int("MYRT_ZEROCOPY", 1, 0, 1) == 1;
+    bool zerocopy = direct && s->opt[kOptZerocopy] != 0;
     for (int32_t k = 0; k < D && zerocopy; ++k) {
         HIP_TRY(hipSetDevice(s->devs[k].device));
         zerocopy = (!out_rgb || hipHostGetDevicePointer((void**)&zc_rgb[k], out_rgb, 0) == hipSuccess) &&
@@ -1997,8 +2057,8 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
     // Launches per replica.  Each batch ends on its slowest tile, so batches cost time
     // (~0.1-0.2 ms each on C3): they are used for progress granularity when a callback is
     // given, and otherwise only to overlap the copy of batch b with the render of b+1.
-    const int32_t nBatches = env_int("MYRT_BATCHES", progress ? kRenderBatches : (zerocopy ? 1 : 2),
-                                     1, kRenderBatches);
+    const int32_t nBatches = s->opt[kOptBatches] > 0 ? (int32_t)s->opt[kOptBatches]
+                                                    : (progress ? kRenderBatches : (zerocopy ? 1 : 2));
 
     // ---- per replica: its chunk list, batch plan, buffers; enqueue everything
     struct Plan { int32_t myFirst, myStep, nChunks, rows, nb, per; std::vector<int32_t> batchRow; };
@@ -2184,7 +2244,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
         }
     }
     double km = 0;
-    int64_t sh = 0, se = 0, st = 0;
+    int64_t sh = 0, se = 0, st = 0, rw = 0;
     for (int32_t k = 0; k < D; ++k) {
         if (plan[k].nb == 0) continue;
         DeviceReplica& r = s->devs[k];
@@ -2197,7 +2257,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
         }
         HIP_TRY(hipEventSynchronize(r.counters_ready));
         const unsigned long long* c = r.host_counters;
-        sh += (int64_t)c[0]; se += (int64_t)c[1]; st += (int64_t)c[kCounterShadowTraced];
+        sh += (int64_t)c[0]; se += (int64_t)c[1]; st += (int64_t)c[kCounterShadowTraced]; rw += (int64_t)c[kCounterTies];
         float ms = 0; (void)hipEventElapsedTime(&ms, r.ev0, r.ev1);
         km = std::max(km, (double)ms);
     }
@@ -2209,6 +2269,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
         stats->primary_rays = (int64_t)rowsTotal * W * n * n;
         stats->shadow_rays = sh; stats->secondary_rays = se; stats->kernel_ms = km;
         stats->shadow_rays_traced = st;
+        stats->rewalked = rw;
         stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return RT_OK;
@@ -2322,11 +2383,13 @@ static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o,
         }
         P.prune_abs = prune_abs_for(s->host, od);
         P.fast_rcp = fast_rcp_for(s->host, 2.0 * dm + 1.0);
+        double oc = 0.0;                      // the wide walk's widening for these origins
+        for (int32_t k = 0; k < 3 * n; ++k) oc = std::isfinite(o[k]) ? std::max(oc, std::fabs(o[k])) : HUGE_VAL;
+        set_wide(s->host, r, P, oc, s->opt[kOptWide] != 0);
     }
     dev::RayBatch B{};
     B.n = n;
-    const char* ue = std::getenv("MYRT_UNIFIED");
-    const bool unified = P.has_tlas && !(ue && ue[0] == '0');
+    const bool unified = P.has_tlas && s->opt[kOptUnified] != 0;
     B.uni = (unified && P.identity) ? 1 : (unified && P.ut) ? 2 : 0;   // the render kernels' walk
     std::vector<void*> allocs;
     auto dalloc = [&](size_t bytes, void** p) -> int32_t {
@@ -2392,13 +2455,13 @@ int32_t rt_debug_wave_times(rt_scene* s, int32_t slot, int32_t cam, int32_t firs
                                         "tools/build_variants.sh)");
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded. Can't render.");
     if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
-    int32_t rc = check_renderable(s->host, cam);
+    int32_t rc = check_renderable(s, cam);
     if (rc != RT_OK) return rc;
     std::lock_guard<std::mutex> lock(s->mu);
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     RenderParams P = make_params(s, r, cam, first, step, d_out_rgb, nullptr);
-    const int bt = block_threads();
+    const int bt = kRenderBlock;
     const int64_t waves = (int64_t)render_grid(P, bt, dev::kTileW).x * (bt / 64);
     if (waves > r.wave_times_cap) {
         (void)hipFree(r.wave_times); r.wave_times = nullptr; r.wave_times_cap = 0;

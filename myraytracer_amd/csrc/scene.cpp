@@ -460,6 +460,164 @@ static int32_t layout_bvh(const RefBVH& b, std::vector<WRec>& recs, EmitLeaf emi
     return (int32_t)recOf[0];
 }
 
+// ------------------------------------------------------------ conservative four-wide tree
+// Identity scenes: the unified TLAS + BLAS tree (TLAS inner records, TLAS leaves = their
+// instances' BLAS roots, BLAS inner records, BLAS leaf runs) collapsed into W4Nodes (layout.h).
+// A node starts from one tree node's children and repeatedly opens the child with the largest
+// surface area while the children fit four slots (the usual BVH2 -> BVH4 collapse); a TLAS leaf
+// with more than four instances is grouped.  Every reference leaf run becomes exactly one slot,
+// and its exact FP64 box is kept in lbox for the walk's exact check (wide.h).  Slot order keeps
+// the tree's left-to-right order.
+namespace {
+struct WItem {
+    double lo[3], hi[3];
+    int32_t ref;        // a tree ref (records / TLAS leaf / BLAS leaf run), unless group >= 0
+    int32_t group;      // >= 0: a synthetic group of items (wide groups)
+};
+struct WideBuilder {
+    HostScene& S;
+    std::vector<std::vector<WItem>> groups;
+    int depth = 0, max_depth = 0;        // wide levels on the current path / deepest
+    explicit WideBuilder(HostScene& s) : S(s) {}
+    bool terminal(const WItem& x) const { return x.group < 0 && x.ref < 0 && (int64_t)~x.ref < S.tlas_leaf_base; }
+    static double area(const WItem& x) {
+        const double dx = x.hi[0] - x.lo[0], dy = x.hi[1] - x.lo[1], dz = x.hi[2] - x.lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    }
+    std::vector<WItem> expand(const WItem& x) const {
+        std::vector<WItem> out;
+        if (x.group >= 0) return groups[x.group];
+        if (x.ref >= 0) {
+            const WRec& r = S.recs[x.ref];
+            for (int c = 0; c < 2; ++c) {
+                WItem w{};
+                for (int k = 0; k < 3; ++k) { w.lo[k] = r.lo[c][k]; w.hi[k] = r.hi[c][k]; }
+                w.ref = r.ref[c];
+                w.group = -1;
+                out.push_back(w);
+            }
+            return out;
+        }
+        for (int64_t e = (int64_t)~x.ref - S.tlas_leaf_base;; ++e) {      // TLAS leaf: instance roots
+            const DInstance& I = S.insts[S.tlas_leaf[e].inst];
+            WItem w{};
+            for (int k = 0; k < 3; ++k) { w.lo[k] = I.root_lo[k]; w.hi[k] = I.root_hi[k]; }
+            w.ref = I.root_ref;
+            w.group = -1;
+            out.push_back(w);
+            if (S.tlas_leaf[e].last) break;
+        }
+        return out;
+    }
+    size_t expand_count(const WItem& x) const {
+        if (x.group >= 0) return groups[x.group].size();
+        if (x.ref >= 0) return 2;
+        size_t n = 0;
+        for (int64_t e = (int64_t)~x.ref - S.tlas_leaf_base;; ++e) { ++n; if (S.tlas_leaf[e].last) break; }
+        return n;
+    }
+    // more than four items: four consecutive groups
+    std::vector<WItem> regroup(const std::vector<WItem>& c) {
+        if (c.size() <= 4) return c;
+        std::vector<WItem> out;
+        const size_t n = c.size();
+        for (size_t g = 0; g < 4; ++g) {
+            const size_t a = n * g / 4, b = n * (g + 1) / 4;
+            if (a == b) continue;
+            if (b - a == 1) { out.push_back(c[a]); continue; }
+            WItem w{};
+            for (int k = 0; k < 3; ++k) { w.lo[k] = kInf; w.hi[k] = -kInf; }
+            std::vector<WItem> part(c.begin() + a, c.begin() + b);
+            for (const WItem& x : part)
+                for (int k = 0; k < 3; ++k) { w.lo[k] = std::fmin(w.lo[k], x.lo[k]); w.hi[k] = std::fmax(w.hi[k], x.hi[k]); }
+            w.ref = 0;
+            w.group = (int32_t)groups.size();
+            groups.push_back(std::move(part));
+            out.push_back(w);
+        }
+        return out;
+    }
+    static float down(double x) {
+        float f = (float)x;
+        if ((double)f > x) f = std::nextafter(f, -HUGE_VALF);
+        return f;
+    }
+    static float up(double x) {
+        float f = (float)x;
+        if ((double)f < x) f = std::nextafter(f, HUGE_VALF);
+        return f;
+    }
+    int32_t build(const WItem& x) {
+        std::vector<WItem> c = regroup(expand(x));
+        for (;;) {                                       // open the largest child that still fits
+            int best = -1;
+            double bestA = -1.0;
+            for (size_t i = 0; i < c.size(); ++i) {
+                if (terminal(c[i])) continue;
+                if (c.size() - 1 + expand_count(c[i]) > 4) continue;
+                const double a = area(c[i]);
+                if (a > bestA) { bestA = a; best = (int)i; }
+            }
+            if (best < 0) break;
+            const std::vector<WItem> e = expand(c[best]);
+            c.erase(c.begin() + best);
+            c.insert(c.begin() + best, e.begin(), e.end());
+        }
+        const int32_t idx = (int32_t)S.wnodes.size();
+        S.wnodes.emplace_back();
+        max_depth = std::max(max_depth, ++depth);
+        int32_t refs[4] = {0, 0, 0, 0};
+        for (size_t i = 0; i < c.size(); ++i) {
+            if (terminal(c[i])) {
+                refs[i] = c[i].ref;
+                double* b = &S.lbox[6 * (size_t)~c[i].ref];
+                for (int k = 0; k < 3; ++k) { b[k] = c[i].lo[k]; b[3 + k] = c[i].hi[k]; }
+                S.wide_leaves++;
+            } else {
+                refs[i] = build(c[i]);                   // preorder: children follow their parent
+            }
+        }
+        W4Node& n = S.wnodes[idx];
+        std::memset(&n, 0, sizeof(n));
+        for (int s = 0; s < 4; ++s) {
+            for (int k = 0; k < 3; ++k) {
+                if (s < (int)c.size()) {
+                    n.lo[k][s] = down(c[s].lo[k]);
+                    n.hi[k][s] = up(c[s].hi[k]);
+                    S.wide_coord = std::fmax(S.wide_coord, std::fmax(std::fabs(c[s].lo[k]), std::fabs(c[s].hi[k])));
+                } else {
+                    n.lo[k][s] = HUGE_VALF;              // empty slot: never hit (wide.h)
+                    n.hi[k][s] = HUGE_VALF;
+                }
+            }
+            n.ref[s] = refs[s];
+        }
+        --depth;
+        return idx;
+    }
+};
+}  // namespace
+
+static void build_wide(HostScene& S) {
+    S.wnodes.clear();
+    S.lbox.assign(6 * S.tris.size(), 0.0);
+    S.wide_leaves = 0;
+    S.wide_coord = 0.0;
+    WideBuilder B(S);
+    WItem root{};
+    for (int k = 0; k < 3; ++k) { root.lo[k] = S.tlas_root_lo[k]; root.hi[k] = S.tlas_root_hi[k]; }
+    root.ref = S.tlas_root_ref;
+    root.group = -1;
+    if (B.terminal(root)) { S.wnodes.clear(); S.lbox.clear(); S.wide_root = -1; return; }
+    S.wnodes.reserve(S.recs.size() / 2 + 16);
+    S.wide_root = B.build(root);
+    // a walk holds at most three deferred slots per wide level on its path (plus slack): it must
+    // fit the device stack (device.h Stack, kStackCap), else the binary walk
+    if (!std::isfinite(S.wide_coord) || 3 * (int64_t)B.max_depth + 2 > kStackCap) {
+        S.wnodes.clear(); S.lbox.clear(); S.wide_root = -1;
+    }
+}
+
 int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err) {
     auto t0 = std::chrono::steady_clock::now();
     const bool trace = std::getenv("MYRT_BUILD_TRACE") != nullptr;   // phase timings on stderr
@@ -972,6 +1130,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
             }
         }
     }
+    if (S.identity) build_wide(S);
     if (S.recs.size() >= (size_t)INT32_MAX || S.tris.size() >= (size_t)INT32_MAX) { err = "scene too large for int32 refs"; return RT_ERR_UNSUPPORTED; }
     if (maxBlasDepth + 1 > 63 || tlasDepth + 1 > 63) {
         err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550, 623)";

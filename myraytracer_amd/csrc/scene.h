@@ -75,6 +75,12 @@ struct HostScene {
     double max_motion = 0.0;               // largest instance + triangle motion-blur offset
     double det_scale = 0.0;                // >= |e1||e2| * ||A||_F over triangle instances: every
                                            // Moeller-Trumbore |det| <= det_scale * |d_world|
+    // ---- conservative FP32 four-wide walk (identity scenes, scene.cpp build_wide)
+    std::vector<W4Node> wnodes;
+    std::vector<double> lbox;              // 6 per TriRec index: exact box of the leaf run starting there
+    int64_t wide_leaves = 0;               // reference leaves under the wide tree
+    int32_t wide_root = -1;                // -1: no wide tree
+    double wide_coord = 0.0;               // largest |coordinate| of any box (wdelta scale)
     // ---- bookkeeping / debug
     int64_t n_meshes = 0, n_tris = 0, n_spheres = 0, n_planes = 0;
     std::vector<uint64_t> inst_bvh_hash;   // per instance: canonical hash of its BLAS

@@ -70,6 +70,7 @@ class RenderStats:                       # Models/RenderStats.swift:8-24 (+ ray 
     milliseconds: float
     kernel_ms: float
     shadow_rays_traced: int = 0          # shadow rays whose any-hit walk ran (<= shadow_rays)
+    rewalked: int = 0                    # closest-hit rays re-walked in reference order (equal-t ties)
 
     @property
     def rays_traced(self) -> int:
@@ -157,6 +158,15 @@ class RayTracerEngine:
     @property
     def handle(self):
         return self._h
+
+    # -- render options (rt_scene_set_option; defaults are the production settings)
+    def set_option(self, name: str, value: int):
+        _check(load_library().rt_scene_set_option(self._h, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        _check(load_library().rt_scene_get_option(self._h, name.encode(), C.byref(v)))
+        return int(v.value)
 
     # -- introspection (RayTracer.swift:52-67)
     def info(self) -> A.rt_scene_info:
@@ -396,7 +406,7 @@ def _stats(st: A.rt_stats) -> RenderStats:
     return RenderStats(int(st.meshes), int(st.triangles), int(st.spheres), int(st.planes),
                        int(st.primary_rays + st.shadow_rays), int(st.primary_rays), int(st.shadow_rays),
                        int(st.secondary_rays), float(st.milliseconds), float(st.kernel_ms),
-                       int(st.shadow_rays_traced))
+                       int(st.shadow_rays_traced), int(st.rewalked))
 
 
 def register_host(arr: np.ndarray):

@@ -73,7 +73,21 @@ def test_error_codes_without_compute():
     m = A.rt_ply_mesh()
     assert lib.rt_ply_load(b"/nonexistent.ply", C.byref(m)) == A.RT_ERR_PLY
     assert lib.rt_version().startswith(b"myraytracer_amd")
-    assert b"(abi 2," in lib.rt_version()          # RT_ABI_VERSION (rtcore.h)
+    assert f"(abi {A.RT_ABI_VERSION},".encode() in lib.rt_version()   # RT_ABI_VERSION (rtcore.h)
+    v = C.c_int64()
+    assert lib.rt_scene_set_option(None, b"wide", 0) == A.RT_ERR_NO_SCENE
+    assert lib.rt_scene_get_option(None, b"wide", C.byref(v)) == A.RT_ERR_NO_SCENE
+
+
+def test_header_declares_the_abi_version_and_struct_sizes():
+    """rtcore.h's RT_ABI_VERSION and the ctypes mirror agree; the structs that grew in version 3
+    (rt_stats.rewalked, rt_scene_info.scratch_bytes) have the header's layout."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "rtcore.h")).read()
+    assert int(re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1)) == A.RT_ABI_VERSION
+    assert C.sizeof(A.rt_stats) == 11 * 8 and A.rt_stats.rewalked.offset == 10 * 8
+    assert C.sizeof(A.rt_scene_info) == 12 * 8 and A.rt_scene_info.scratch_bytes.offset == 11 * 8
 
 
 def test_product_fails_loudly_without_gpu():

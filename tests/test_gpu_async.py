@@ -84,14 +84,13 @@ def test_pipelined_frames_against_the_oracle():
     eng.close()
 
 
-@pytest.mark.parametrize("full_flights", ["0", "2", "4"])
-def test_full_trace_renders_in_flight(monkeypatch, full_flights):
+@pytest.mark.parametrize("full_flights", [0, 2, 4])
+def test_full_trace_renders_in_flight(full_flights):
     """Dielectrics / area lights take the full trace() passes (render_full.h), whose scratch
     (event counts, jitter prefixes, hit log, node records) belongs to a stream: submitted renders
-    take slot q % MYRT_FULL_FLIGHTS's stream and scratch, so up to that many overlap (0: all on
+    take slot q % full_flights's stream and scratch (render option), so up to that many overlap (0: all on
     the replica's stream, in order).  Two cameras, chunk selections and glass at once, waits in
     a ring; every frame equals rt_render_ex's."""
-    monkeypatch.setenv("MYRT_FULL_FLIGHTS", full_flights)
     from test_gpu_features import _area_scene
     sc = _area_scene(96, 64)                                 # area lights (render_full)
     sc.objects[3].material = "3"                             # + glass
@@ -100,6 +99,7 @@ def test_full_trace_renders_in_flight(monkeypatch, full_flights):
     sc.cameras.append(c2)
     W, H = sc.cameras[0].image_resolution
     eng = M.RayTracerEngine(sc)
+    eng.set_option("full_flights", full_flights)
     jobs = [(0, 0, 1), (1, 0, 1), (0, 1, 3), (1, 2, 2)]
     want = [_sync(eng, *j, H, W) for j in jobs]
     Q = 6
@@ -147,8 +147,8 @@ def test_submit_errors():
     eng.close()
 
 
-def test_failed_replica_launch_drains_and_frees_the_slot(monkeypatch):
-    """A launch that fails on replica k > 0 (forced: MYRT_DEBUG_FAIL_REPLICA) must not leave
+def test_failed_replica_launch_drains_and_frees_the_slot():
+    """A launch that fails on replica k > 0 (forced: option debug_fail_replica) must not leave
     replicas 0..k-1 writing into the caller's buffers behind an error: they are drained before
     rt_render_submit returns, and the slot is free again (every slot still takes a render)."""
     sc = scenes.scaled(scenes.scene_c2(inline=True), 96, 72)
@@ -157,7 +157,7 @@ def test_failed_replica_launch_drains_and_frees_the_slot(monkeypatch):
     want = _sync(eng, 0, 0, 1, H, W)
     out = M.pinned_array((H, W, 4), np.uint8)
     out.fill(0)
-    monkeypatch.setenv("MYRT_DEBUG_FAIL_REPLICA", "1")
+    eng.set_option("debug_fail_replica", 1)
     with pytest.raises(M.RenderError) as e:
         eng.submit_into(0, 0, 1, rgba=out, frame_layout=True)
     assert e.value.code == A.RT_ERR_DEVICE and "injected" in str(e.value)
@@ -170,7 +170,7 @@ def test_failed_replica_launch_drains_and_frees_the_slot(monkeypatch):
         rows[8 * c: 8 * c + 8] = True
     snap = out.copy()
     assert np.array_equal(snap[rows], want[1][rows]) and np.all(snap[~rows] == 0)
-    monkeypatch.delenv("MYRT_DEBUG_FAIL_REPLICA")
+    eng.set_option("debug_fail_replica", -1)
     outs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(A.RT_MAX_IN_FLIGHT)]
     ts = [eng.submit_into(0, 0, 1, rgba=o, frame_layout=True) for o in outs]
     for t, o in zip(ts, outs):
@@ -210,15 +210,15 @@ def test_concurrent_waits_on_one_ticket():
     eng.close()
 
 
-@pytest.mark.parametrize("queue", ["0", "1"])
-def test_pipelined_mirror_frames_against_the_oracle(monkeypatch, queue):
+@pytest.mark.parametrize("queue", [0, 1])
+def test_pipelined_mirror_frames_against_the_oracle(queue):
     """Mirror frames in flight (each slot has its own bounce queues and counters): every frame
     equals the oracle and carries the oracle's secondary-ray count."""
-    monkeypatch.setenv("MYRT_QUEUE", queue)
     from test_gpu_features import _mirror_corridor
     sc = _mirror_corridor(6, 80, 56)
     ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
     eng = M.RayTracerEngine(sc)
+    eng.set_option("queue", queue)
     Q = A.RT_MAX_IN_FLIGHT
     fbs = [M.pinned_array((56, 80, 4), np.uint8) for _ in range(Q)]
     pend = []

@@ -17,8 +17,10 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
-def _compare(sc, chunk_first=0, chunk_step=1, cam=0):
+def _compare(sc, chunk_first=0, chunk_step=1, cam=0, options=None):
     eng = M.RayTracerEngine(sc)
+    for k, v in (options or {}).items():                 # render options (rt_scene_set_option)
+        eng.set_option(k, v)
     rgb, rgba, st = eng.render_rows(cam, chunk_first, chunk_step, True)
     ref, ref8, ost = oracle.OracleScene(sc).render(cam, chunk_first, chunk_step, threads=0, rgba=True)
     diff = np.abs(rgb - ref)
@@ -116,61 +118,53 @@ def test_area_lights_with_dielectric_and_mesh():
     _compare(sc)
 
 
-@pytest.mark.parametrize("slots, nodeshade", [("auto", "1"), ("auto", "0"), ("1", "1"), ("8", "1"), ("0", "1")])
-def test_area_light_hit_log(monkeypatch, slots, nodeshade):
+@pytest.mark.parametrize("slots, nodeshade", [(-1, 1), (-1, 0), (1, 1), (8, 1), (0, 1)])
+def test_area_light_hit_log(slots, nodeshade):
     """render_full reads the closest hits k_events logged instead of walking them again
-    (RenderParams::hits), and k_shade shades the logged hits node-parallel (MYRT_NODESHADE=1,
+    (RenderParams::hits), and k_shade shades the logged hits node-parallel (option nodeshade = 1,
     default) or render_full does (0): the default log holds every walk of the paths here, 8 or
     1 slots send longer paths past the log to the fallback walk, 0 turns the log off.  Glass, mirror and a rough
     dielectric give paths of up to 2^5 - 1 walks; four samples per pixel."""
-    if slots == "auto":                                  # sized to the scene's path trees (here 31 per sample)
-        monkeypatch.delenv("MYRT_HITLOG", raising=False)
-    else:
-        monkeypatch.setenv("MYRT_HITLOG", slots)
-    monkeypatch.setenv("MYRT_NODESHADE", nodeshade)   # logged hits shaded node-parallel (k_shade) or by render_full
+    # hitlog -1: sized to the scene's path trees (here 31 per sample); nodeshade: logged hits shaded
+    # node-parallel (k_shade) or by render_full
     sc = _area_scene(88, 64, spp=4)
     sc.objects[1].material = "3"
     sc.objects[2].material = "2"
     sc.objects[3].material = "5"
     sc.max_recursion_depth = 4
-    st = _compare(sc)
+    st = _compare(sc, options={"hitlog": slots, "nodeshade": nodeshade})
     assert st.secondary_rays > 0
 
 
-@pytest.mark.parametrize("levels, ppw", [("1", "4"), ("1", "1"), ("1", "64"), ("0", "4")])
+@pytest.mark.parametrize("levels, ppw", [(1, 4), (1, 1), (1, 64), (0, 4)])
 @pytest.mark.parametrize("spp, depth, glass", [(1, 4, True), (4, 3, True), (1, 5, True), (4, 4, False), (9, 2, True)])
-def test_area_light_level_passes(monkeypatch, levels, ppw, spp, depth, glass):
-    """Breadth-first events passes (render_full.h k_level, MYRT_LEVELS=1, default) against the
+def test_area_light_level_passes(levels, ppw, spp, depth, glass):
+    """Breadth-first events passes (render_full.h k_level, option levels = 1, default) against the
     depth-first k_events (0): no rough material, so the tree's walks may run level by level;
     heap-indexed trees with glass (2^(D+1) - 1 nodes per traced sample), chains without; 4 and 9
     samples per pixel give several trees per pixel; depth 5 with one sample fills 63 of the 64
     log slots.  k_jofs must reproduce the depth-first jitterIndex offsets exactly.  A wave runs 1,
-    4 (default) or all of a level's node positions (MYRT_TREE_PPW)."""
-    monkeypatch.setenv("MYRT_LEVELS", levels)
-    monkeypatch.setenv("MYRT_TREE_PPW", ppw)
-    monkeypatch.delenv("MYRT_HITLOG", raising=False)
+    4 (default) or all of a level's node positions (option tree_ppw)."""
     sc = _area_scene(72, 56, spp=spp)
     sc.objects[1].material = "3" if glass else "2"
     sc.objects[2].material = "4"
     sc.objects[3].material = "3" if glass else "4"
     sc.max_recursion_depth = depth
-    st = _compare(sc)
+    st = _compare(sc, options={"levels": levels, "tree_ppw": ppw})
     assert st.secondary_rays > 0
 
 
-@pytest.mark.parametrize("levels", ["1", "0"])
+@pytest.mark.parametrize("levels", [1, 0])
 @pytest.mark.parametrize("spp, depth", [(1, 4), (4, 3)])
-def test_dielectric_level_passes_without_area_lights(monkeypatch, levels, spp, depth):
+def test_dielectric_level_passes_without_area_lights(levels, spp, depth):
     """Glass + mirror + conductor with point lights only: the level passes and node shading
-    (MYRT_LEVELS=1, default) or render_full alone (0).  No jitterIndex here, so no events prefix."""
-    monkeypatch.setenv("MYRT_LEVELS", levels)
-    monkeypatch.delenv("MYRT_HITLOG", raising=False)
+    (option levels = 1, default) or render_full alone (0).  No jitterIndex here, so no events prefix."""
     sc = _primitives_scene(80, 60)
     sc.cameras[0].num_samples = spp
     sc.objects[1].material = "3"
     sc.objects[3].material = "3"
     sc.max_recursion_depth = depth
-    st = _compare(sc)
+    st = _compare(sc, options={"levels": levels})
     assert st.secondary_rays > 0
 
 
@@ -290,17 +284,16 @@ def test_deep_recursion_with_glass_and_area_light():
     _compare(sc)
 
 
-def test_deep_recursion_batched_launches(monkeypatch):
+def test_deep_recursion_batched_launches():
     """Frames whose deep levels exceed one launch's buffer are rendered in chunk batches
     (render.hip launch_full): 16 tiles x 64 lanes x 284 levels x 128 B = 37 MB per chunk,
     so a 40 MB cap gives one chunk per launch.  The result must not depend on the batching."""
-    monkeypatch.setenv("MYRT_DEEP_CAP_MB", "40")
-    _compare(_mirror_corridor(300, 128, 64), chunk_first=1, chunk_step=2)
+    _compare(_mirror_corridor(300, 128, 64), chunk_first=1, chunk_step=2, options={"deep_cap_mb": 40})
 
 
-def test_deep_recursion_refused_past_the_buffer(monkeypatch):
-    monkeypatch.setenv("MYRT_DEEP_CAP_MB", "1")
+def test_deep_recursion_refused_past_the_buffer():
     eng = M.RayTracerEngine(_mirror_corridor(300, 128, 64))
+    eng.set_option("deep_cap_mb", 1)
     with pytest.raises(M.RenderError) as e:
         eng.render(0)
     assert e.value.code == A.RT_ERR_UNSUPPORTED
@@ -316,28 +309,29 @@ def _rough_mirror_scene(w=128, h=96):
     return sc
 
 
-@pytest.mark.parametrize("queue", ["0", "1"])
-def test_queued_bounces_against_the_oracle(monkeypatch, queue):
-    """Mirror/conductor scenes through the compacted bounce render (MYRT_QUEUE=1, the default:
+@pytest.mark.parametrize("queue", [0, 1])
+def test_queued_bounces_against_the_oracle(queue):
+    """Mirror/conductor scenes through the compacted bounce render (option queue = 1, opt-in:
     primary pass + one k_bounce launch per level, rays resolved backward through their queue
-    records) and through the bounce megakernel (0): both equal the oracle's recursion
+    records) and through the bounce megakernel (0, the default): both equal the oracle's recursion
     (Object+Extension.swift:189-206, 252-283).  Covers the general walk (a transformed
     instance), rough mirrors, spp 3 (one traced sample divided by 3), the unified walk with 15
     queue levels, chunk selections, and several replicas."""
-    monkeypatch.setenv("MYRT_QUEUE", queue)
+    opt = {"queue": queue}
     sc = _rough_mirror_scene()
-    st = _compare(sc)
+    st = _compare(sc, options=opt)
     assert st.secondary_rays > 0
     sc.cameras[0].num_samples = 3
-    _compare(sc)
-    st = _compare(_mirror_corridor(15, 48, 36))
+    _compare(sc, options=opt)
+    st = _compare(_mirror_corridor(15, 48, 36), options=opt)
     assert st.secondary_rays > 10 * 48 * 36 // 2
-    _compare(_mirror_corridor(12, 48, 36), chunk_first=1, chunk_step=3)
+    _compare(_mirror_corridor(12, 48, 36), chunk_first=1, chunk_step=3, options=opt)
     # 3 chunks -> rt_render_ex's two staged launches of different sizes share one queue arena
-    _compare(_mirror_corridor(8, 64, 40), chunk_first=0, chunk_step=2)
+    _compare(_mirror_corridor(8, 64, 40), chunk_first=0, chunk_step=2, options=opt)
     sc = _mirror_corridor(8, 56, 40)
     ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
     eng = M.RayTracerEngine(sc, devices=[0, 0, 0])
+    eng.set_option("queue", queue)
     for _ in range(2):                                 # queue words must be back at zero
         rgb, rgba, st = eng.render_rows(0, 0, 1, True)
         assert float(np.abs(rgb - ref).max()) <= TOL and np.array_equal(rgba, ref8)

@@ -57,10 +57,13 @@ def _assert_frame(rgb, rgba, ref, ref8):
         assert np.array_equal(rgba, ref8), f"RGBA8 differs on {int((rgba != ref8).any(-1).sum())} px"
 
 
-def test_c3_full_frame_bench_path(c3_ply, monkeypatch):
-    monkeypatch.delenv("MYRT_PATH", raising=False)
+@pytest.mark.parametrize("wide", [1, 0])
+def test_c3_full_frame_bench_path(c3_ply, wide):
+    """The bench's own call on the full C3 frame, through the four-wide walk (default) and the
+    binary walk (render option wide = 0)."""
     sc, ref, ref8, ost = c3_ply
     eng = M.RayTracerEngine(sc)
+    eng.set_option("wide", wide)
     H, W = ref.shape[:2]
     rgba = M.pinned_array((H, W, 4), np.uint8)
     rgb = M.pinned_array((H, W, 3), np.float64)
@@ -75,12 +78,11 @@ def test_c3_full_frame_bench_path(c3_ply, monkeypatch):
     eng.close()
 
 
-def test_c3_full_frames_in_flight_bench_path(c3_ply, monkeypatch):
+def test_c3_full_frames_in_flight_bench_path(c3_ply):
     """bench.py's timed loop exactly: frames submitted with 4 renders in flight
     (engine.frame_pipeline -> rt_render_submit / rt_render_wait), frame k into page-locked
     framebuffer k mod 4; every delivered frame equals the oracle's RGBA8 and its counts."""
     import collections
-    monkeypatch.delenv("MYRT_PATH", raising=False)
     sc, ref, ref8, ost = c3_ply
     eng = M.RayTracerEngine(sc)
     H, W = ref.shape[:2]
@@ -109,9 +111,8 @@ def test_c3_full_frames_in_flight_bench_path(c3_ply, monkeypatch):
     eng.close()
 
 
-def test_c3_full_frame_device_path(c3_ply, monkeypatch):
+def test_c3_full_frame_device_path(c3_ply):
     import torch
-    monkeypatch.delenv("MYRT_PATH", raising=False)
     sc, ref, ref8, _ = c3_ply
     eng = M.RayTracerEngine(sc)
     H, W = ref.shape[:2]
@@ -124,10 +125,9 @@ def test_c3_full_frame_device_path(c3_ply, monkeypatch):
     eng.close()
 
 
-def test_c4_eight_replicas_full_c3(c3_ply, monkeypatch):
+def test_c4_eight_replicas_full_c3(c3_ply):
     """configs[3]: the C3 frame split over 8 replicas (8-row chunk c on replica c mod 8; here all
     on the one GPU of the box), gathered by rt_render into one page-locked frame."""
-    monkeypatch.delenv("MYRT_PATH", raising=False)
     sc, ref, ref8, ost = c3_ply
     H, W = ref.shape[:2]
     eng8 = M.RayTracerEngine(sc, devices=[0] * 8)
@@ -182,7 +182,6 @@ def test_frame_layout_gathers_disjoint_selections(devices):
 
 def _bench(args, env_extra):
     env = dict(os.environ, **env_extra)
-    env.pop("MYRT_PATH", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
                        timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -226,14 +225,13 @@ def test_bench_strong_split_eight_ranks_on_one_gpu():
 
 @pytest.mark.timeout(400)
 @pytest.mark.parametrize("name", ["c3i", "c3g", "c3d"])
-def test_general_path_bench_configs_full_frame(scene_dir, name, monkeypatch):
+def test_general_path_bench_configs_full_frame(scene_dir, name):
     """The bench's general-path configs on full 1920x1080 frames against the oracle: C3i (C3's
     geometry as 25 transformed mesh instances: the literal TLAS->BLAS walk, RTContext.swift:
     619-720) and C3g (glass spheres + two area lights: render_full with k_events/k_jscan,
     Object+Extension.swift:145-251) and C3d (the glass spheres with the point light only: level
     passes + node shading without events), through bench.py's call (RGBA8 into page-locked
     memory) and the FP64 frame."""
-    monkeypatch.delenv("MYRT_PATH", raising=False)
     make = {"c3i": scenes.scene_c3_instanced, "c3g": scenes.scene_c3_glass,
             "c3d": lambda path_dir: scenes.scene_c3_glass(path_dir=path_dir, area_lights=False)}[name]
     sc = make(path_dir=scene_dir)

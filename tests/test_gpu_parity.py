@@ -4,7 +4,6 @@ Bar (BASELINE.json north_star): per-channel L-inf <= 1e-5 on the FP64 framebuffe
 plus exact RGBA8 equality.  Every test renders through libmyrt.so on cuda:0.
 """
 import copy
-import os
 
 import numpy as np
 import pytest
@@ -17,15 +16,10 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5   # per-channel L-inf, north_star
 
 
-@pytest.fixture(params=["mega", "wave"], autouse=True)
-def render_path(request, monkeypatch):
-    """Every parity test runs on both device pipelines (megakernel and wavefront)."""
-    monkeypatch.setenv("MYRT_PATH", request.param)
-    return request.param
-
-
-def _compare(sc, chunk_first=0, chunk_step=1, cam=0, tol=TOL, check_rgba=True):
+def _compare(sc, chunk_first=0, chunk_step=1, cam=0, tol=TOL, check_rgba=True, options=None):
     eng = M.RayTracerEngine(sc)
+    for k, v in (options or {}).items():
+        eng.set_option(k, v)
     rgb, rgba, st = eng.render_rows(cam, chunk_first, chunk_step, True)
     o = oracle.OracleScene(sc)
     ref, ref8, ost = o.render(cam, chunk_first, chunk_step, threads=0, rgba=True)
@@ -38,11 +32,8 @@ def _compare(sc, chunk_first=0, chunk_step=1, cam=0, tol=TOL, check_rgba=True):
     assert st.primary_rays == ost.primary_rays
     assert st.shadow_rays == ost.shadow_rays, (st.shadow_rays, ost.shadow_rays)
     assert st.secondary_rays == ost.secondary_rays, (st.secondary_rays, ost.secondary_rays)
-    # shadow walks actually run: the megakernels skip the ones whose result the reference
-    # discards (N.L <= 0); the wavefront pipeline traces every cast ray
-    assert ost.shadow_rays_used <= st.shadow_rays_traced <= st.shadow_rays
-    if os.environ.get("MYRT_PATH") != "wave":
-        assert st.shadow_rays_traced == ost.shadow_rays_used, (st.shadow_rays_traced, ost.shadow_rays_used)
+    # shadow walks actually run: the kernels skip the ones whose result the reference discards (N.L <= 0)
+    assert st.shadow_rays_traced == ost.shadow_rays_used, (st.shadow_rays_traced, ost.shadow_rays_used)
     eng.close()
     return linf, st
 
@@ -224,12 +215,10 @@ def _ref_counts_case(name):
 
 
 @pytest.mark.parametrize("case", ["c2", "c3", "instances", "mirror"])
-def test_reference_order_work_counts_match_oracle(case, render_path):
+def test_reference_order_work_counts_match_oracle(case):
     """The GPU's reference-order tally (the roofline's algorithmic bytes)
     equals the oracle's instrumented counts exactly."""
     import torch
-    if render_path != "mega":
-        pytest.skip("counting launch is path-independent (always the megakernel)")
     sc, first, step = _ref_counts_case(case)
     eng = M.RayTracerEngine(sc)
     W, H = sc.cameras[0].image_resolution

@@ -6,7 +6,13 @@ Camera rays almost never have a zero direction component, so the frame tests exe
 axis-aligned and signed-zero directions (1/d = +-inf, NaN slab products), rays
 through shared vertices and edges of a grid (equal-t triangles: first visited wins, H2),
 grazing rays along box faces, and rays mixed in one wave with ordinary ones.  Hits must be
-bit-identical: t, world point, world normal and material."""
+bit-identical: t, world point, world normal and material.
+
+Identity scenes run on three walks (render options, rt_scene_set_option): the conservative
+four-wide FP32 walk (wide.h, the default), the binary unified walk (wide = 0) and the nested
+walk of intersectTLAS (unified = 0)."""
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -15,6 +21,18 @@ from myraytracer_amd import scenes
 import oracle
 
 pytestmark = pytest.mark.gpu
+
+# walk name -> render options (identity scenes: wide / unified / general; instanced scenes:
+# transformed / general)
+WALKS = {"wide": {}, "unified": {"wide": 0}, "general": {"unified": 0},
+         "transformed": {}, "nested": {"unified_transformed": 0}}
+
+
+def _engine(sc, walk):
+    eng = M.RayTracerEngine(sc)
+    for k, v in WALKS[walk].items():
+        eng.set_option(k, v)
+    return eng
 
 
 def _axis_dirs():
@@ -42,8 +60,8 @@ def _ray_set(center, radius, n_random, seed):
     return O, D
 
 
-def _check_closest(sc, O, D, tmin=None, time=None):
-    eng = M.RayTracerEngine(sc)
+def _check_closest(sc, O, D, tmin=None, time=None, walk="wide"):
+    eng = _engine(sc, walk)
     tg, pg, ng, mg = eng.trace_rays(O, D, tmin, time)
     to, po, no, mo = oracle.OracleScene(sc).trace_rays(O, D, tmin, time)
     eng.close()
@@ -54,8 +72,8 @@ def _check_closest(sc, O, D, tmin=None, time=None):
     return hit
 
 
-def _check_occluded(sc, O, D, tmax, time=None):
-    eng = M.RayTracerEngine(sc)
+def _check_occluded(sc, O, D, tmax, time=None, walk="wide"):
+    eng = _engine(sc, walk)
     g = eng.occluded_rays(O, D, tmax, time)
     o = oracle.OracleScene(sc).occluded_rays(O, D, tmax, time)
     eng.close()
@@ -63,21 +81,23 @@ def _check_occluded(sc, O, D, tmax, time=None):
     return o
 
 
-@pytest.mark.parametrize("walk", ["unified", "general"])
-def test_c2_random_and_axis_rays(walk, monkeypatch):
-    monkeypatch.setenv("MYRT_UNIFIED", "1" if walk == "unified" else "0")
+@pytest.mark.parametrize("walk", ["wide", "unified", "general"])
+def test_c2_random_and_axis_rays(walk):
     sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
     O, D = _ray_set(np.array([0.0, 0.0, 0.0]), 2.5, 4000, 7)
-    hit = _check_closest(sc, O, D)
+    hit = _check_closest(sc, O, D, walk=walk)
     assert 0.2 < hit.mean() < 0.95
     tmax = np.random.RandomState(3).uniform(0.05, 4.0, size=len(O))
-    occ = _check_occluded(sc, O, D, tmax)
+    occ = _check_occluded(sc, O, D, tmax, walk=walk)
     assert 0.05 < occ.mean() < 0.95
 
 
-def test_grid_vertices_edges_and_faces():
+@pytest.mark.parametrize("walk", ["wide", "unified"])
+def test_grid_vertices_edges_and_faces(walk):
     """Vertical rays through heightfield grid vertices, edge midpoints and cell centres:
-    1/d has +-inf components and several triangles share the exact hit."""
+    1/d has +-inf components and several triangles share the exact hit.  Then the same points
+    from tilted directions (every 1/d finite: the four-wide walk takes them) - rays through
+    shared vertices and edges whose triangles may meet at the same t."""
     hp, hf = scenes.heightfield(64, 20.0, 2.0, 5)
     hp32 = hp.astype(np.float32).astype(np.float64)
     mesh = M.Mesh(id=1, material="1", positions=hp32, indices=hf.astype(np.int32), indices_one_based=False,
@@ -91,26 +111,29 @@ def test_grid_vertices_edges_and_faces():
     pts = np.concatenate([verts, 0.5 * (a + b), 0.5 * (b + c), (a + b + c) / 3.0])
     O = pts + np.array([0.0, 10.0, 0.0])
     D = np.tile([0.0, -1.0, 0.0], (len(O), 1))
-    hit = _check_closest(sc, O, D)
+    hit = _check_closest(sc, O, D, walk=walk)
     # MT is not watertight: exactly on shared vertices/edges both triangles can reject the
     # ray (u, v rounding), in the reference as here; the centroids always hit
     assert hit[-300:].all() and hit.mean() > 0.25
+    Dt = np.array([0.3, -1.0, 0.2]) / np.linalg.norm([0.3, -1.0, 0.2])
+    Ot = pts - 10.0 * Dt
+    _check_closest(sc, Ot, np.tile(Dt, (len(Ot), 1)), walk=walk)
+    _check_occluded(sc, Ot, np.tile(Dt, (len(Ot), 1)), np.full(len(Ot), 9.999), walk=walk)
     # grazing: rays in the plane of the grid's bounding faces, along +x and -z
     lo, hi = hp32.min(0), hp32.max(0)
     ys = np.linspace(lo[1], hi[1], 40)
     Og = np.concatenate([np.stack([np.full(40, lo[0] - 1), ys, np.full(40, lo[2])], 1),
                          np.stack([np.full(40, hi[0]), ys, np.full(40, hi[2] + 1)], 1)])
     Dg = np.concatenate([np.tile([1.0, 0.0, 0.0], (40, 1)), np.tile([0.0, 0.0, -1.0], (40, 1))])
-    _check_closest(sc, Og, Dg)
-    _check_occluded(sc, O, D, np.full(len(O), 9.999))
+    _check_closest(sc, Og, Dg, walk=walk)
+    _check_occluded(sc, O, D, np.full(len(O), 9.999), walk=walk)
 
 
-@pytest.mark.parametrize("walk", ["transformed", "general"])
-def test_instances_transforms_and_primitives(walk, monkeypatch):
+@pytest.mark.parametrize("walk", ["transformed", "nested"])
+def test_instances_transforms_and_primitives(walk):
     """Transformed mesh instances, spheres, planes and a triangle: the unified transformed walk
     (one stack, per-instance ray switches at marker entries, device.h ut_walk) and the nested
     general walk both give the oracle's intersectTLAS / occludedTLAS bit for bit."""
-    monkeypatch.setenv("MYRT_UT", "1" if walk == "transformed" else "0")
     sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
     base = sc.objects[0]
     sc.objects = [base,
@@ -120,13 +143,12 @@ def test_instances_transforms_and_primitives(walk, monkeypatch):
                   M.Plane(center=(0.0, -1.5, 0.0), normal=(0.0, 1.0, 0.0), material="1"),
                   M.Triangle(vertices=((-3, -1, -3), (3, -1, -3), (0, 2, -3.5)), material="1")]
     O, D = _ray_set(np.array([0.5, 0.0, 0.0]), 4.0, 3000, 21)
-    _check_closest(sc, O, D)
-    _check_occluded(sc, O, D, np.random.RandomState(5).uniform(0.1, 6.0, size=len(O)))
+    _check_closest(sc, O, D, walk=walk)
+    _check_occluded(sc, O, D, np.random.RandomState(5).uniform(0.1, 6.0, size=len(O)), walk=walk)
 
 
-@pytest.mark.parametrize("walk", ["transformed", "general"])
-def test_motion_blur_times_and_tmin(walk, monkeypatch):
-    monkeypatch.setenv("MYRT_UT", "1" if walk == "transformed" else "0")
+@pytest.mark.parametrize("walk", ["transformed", "nested"])
+def test_motion_blur_times_and_tmin(walk):
     sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
     base = sc.objects[0]
     base.motion_blur = (0.0, 0.2, 0.0)
@@ -134,7 +156,7 @@ def test_motion_blur_times_and_tmin(walk, monkeypatch):
                                        transform=M.translation(0.5, 0.0, 0.5), motion_blur=(0.3, 0.0, 0.0))]
     O, D = _ray_set(np.array([0.0, 0.0, 0.0]), 2.5, 2000, 9)
     rng = np.random.RandomState(2)
-    _check_closest(sc, O, D, tmin=rng.uniform(0.0, 0.5, size=len(O)), time=rng.uniform(0, 1, size=len(O)))
+    _check_closest(sc, O, D, tmin=rng.uniform(0.0, 0.5, size=len(O)), time=rng.uniform(0, 1, size=len(O)), walk=walk)
 
 
 def _rotation(rng):
@@ -146,15 +168,14 @@ def _rotation(rng):
                      [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
 
 
-@pytest.mark.parametrize("walk", ["unified", "general"])
-def test_near_degenerate_grazing_hits_and_the_pruning_margin(walk, monkeypatch):
+@pytest.mark.parametrize("walk", ["wide", "unified", "general"])
+def test_near_degenerate_grazing_hits_and_the_pruning_margin(walk):
     """Large, nearly coplanar triangles and rays grazing them through a corner (|det| just
     above eps): Moeller-Trumbore's t then carries an error of up to ~1e-4 relative and can
     undercut the entry distance of the triangle's own box - far beyond the round-1 margin
     (1e-7 rel + 1e-9 diag), measured on CPU.  The margin now bounds that error
     (scene.cpp, "pruning margin"), so pruning still never drops a node whose triangle the
     reference would accept: hits stay bit-identical to the unpruned oracle."""
-    monkeypatch.setenv("MYRT_UNIFIED", "1" if walk == "unified" else "0")
     rng = np.random.default_rng(17)
     R0 = _rotation(rng)
     V, F, corners = [], [], []
@@ -183,11 +204,55 @@ def test_near_degenerate_grazing_hits_and_the_pruning_margin(walk, monkeypatch):
         O.append(tgt - d * 10 ** rng.uniform(0, 3))
         D.append(d)
     O, D = np.array(O), np.array(D)
-    hit = _check_closest(sc, O, D)
+    hit = _check_closest(sc, O, D, walk=walk)
     assert hit.mean() > 0.3
     t, *_ = oracle.OracleScene(sc).trace_rays(O, D)
     tmax = np.where(np.isfinite(t), t * (1 + rng.choice([-1e-12, 1e-12], size=len(t))), 1e3)
-    _check_occluded(sc, O, D, tmax)
+    _check_occluded(sc, O, D, tmax, walk=walk)
+
+
+def _twin_meshes():
+    """Two meshes holding the SAME triangles (same vertices, same order) with different
+    materials: every hit is an exact tie between two instances, and the reference keeps the
+    first it visits (strict t < hit.t, RTContext.swift:494)."""
+    hp, hf = scenes.heightfield(24, 8.0, 1.0, 3)
+    hp32 = hp.astype(np.float32).astype(np.float64)
+    a = M.Mesh(id=1, material="1", positions=hp32, indices=hf.astype(np.int32), indices_one_based=False,
+               shading_mode="flat")
+    b = M.Mesh(id=2, material="2", positions=hp32.copy(), indices=hf.astype(np.int32)[:, [0, 1, 2]],
+               indices_one_based=False, shading_mode="smooth")
+    sc = scenes.scaled(scenes.scene_c1(8, 8), 48, 40)
+    sc.materials = [sc.materials[0], dataclasses.replace(sc.materials[0], diffuse=(0.1, 0.9, 0.2))]
+    sc.objects = [a, b]
+    sc.cameras[0].position = (0.5, 7.0, 7.5)
+    sc.cameras[0].gaze_point = (0.0, 0.0, 0.0)
+    sc.point_lights[0].position = (1.0, 9.0, 2.0)
+    return sc, hp32
+
+
+@pytest.mark.parametrize("walk", ["wide", "unified"])
+def test_equal_t_ties_between_instances(walk):
+    """Every hit of the twin-mesh scene is an exact tie: the four-wide walk must hand each such
+    ray to the reference-order walk (rewalked > 0) and return the reference's instance -
+    material, point and normal (flat vs smooth) tell the two apart."""
+    sc, hp = _twin_meshes()
+    rng = np.random.RandomState(4)
+    D = rng.normal(size=(3000, 3)) * np.array([0.4, 1.0, 0.4]) - np.array([0.0, 2.0, 0.0])
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    lo, hi = hp.min(0), hp.max(0)
+    tgt = rng.uniform(lo, hi, size=(3000, 3))
+    O = tgt - 12.0 * D
+    hit = _check_closest(sc, O, D, walk=walk)
+    assert hit.mean() > 0.5
+    eng = _engine(sc, walk)
+    rgb, rgba, st = eng.render_rows(0, 0, 1, True)
+    ref, ref8, _ = oracle.OracleScene(sc).render(0, 0, 1, threads=0, rgba=True)
+    eng.close()
+    assert float(np.abs(rgb - ref).max()) <= 1e-5 and np.array_equal(rgba, ref8)
+    if walk == "wide":
+        assert st.rewalked > 0, "no tie was handed to the reference-order walk"
+    else:
+        assert st.rewalked == 0
 
 
 def test_fast_reciprocal_is_ieee_division():

@@ -8,7 +8,7 @@ C=myraytracer_amd/csrc
 while [ $# -ge 2 ]; do
   name="$1"; flags="$2"; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $flags \
-    -o "build_variants/libmyrt_${name}.so" $C/render.hip $C/wavefront.hip $C/scene.cpp $C/ply.cpp $C/sceneio.cpp &
+    -o "build_variants/libmyrt_${name}.so" $C/render.hip $C/scene.cpp $C/ply.cpp $C/sceneio.cpp &
 done
 wait
 ls -la build_variants

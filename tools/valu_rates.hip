@@ -31,6 +31,17 @@ __global__ __launch_bounds__(256) void k(double* out, float* outf, double a, dou
             if (OP == 11) asm volatile("v_pk_add_f32 %0, %0, %0" : "+v"(x[c]));
             if (OP == 12) asm volatile("v_max_f32 %0, %0, %1" : "+v"(f[c]) : "v"((float)b));
             if (OP == 13) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(f[c]) : "v"((float)b));
+            if (OP == 15) asm volatile("v_min3_f32 %0, %0, %1, %1" : "+v"(f[c]) : "v"((float)b));
+            if (OP == 16) asm volatile("v_max3_f32 %0, %0, %1, %1" : "+v"(f[c]) : "v"((float)b));
+            if (OP == 17) asm volatile("v_min_u32 %0, %0, %1" : "+v"(iv[c]) : "v"(f[c]));
+            if (OP == 18) asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(f[c]) : "v"(iv[c]));
+            if (OP == 19) asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(x[c]));
+            if (OP == 20) asm volatile("v_cmp_lt_f32 vcc, %0, %1" :: "v"(f[c]), "v"((float)b) : "vcc");
+            if (OP == 21) asm volatile("v_min_f32 %0, %0, %1" : "+v"(f[c]) : "v"((float)b));
+            if (OP == 22) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f[c]) : "v"((float)b), "s"((float)a));
+            if (OP == 23) asm volatile("v_med3_f32 %0, %0, %1, %1" : "+v"(f[c]) : "v"((float)b));
+            if (OP == 24) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f[c]) : "v"(x[c]));
+            if (OP == 25) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(f[c]) : "v"((float)b));
         }
     }
     double s = 0;
@@ -64,5 +75,9 @@ int main() {
     run<6>("v_cndmask_b32", o, of); run<7>("v_add_f32", o, of); run<8>("v_add_u32", o, of);
     run<9>("v_rcp_f64", o, of); run<10>("v_cmp_f64(sgpr)", o, of); run<11>("v_pk_add_f32", o, of);
     run<12>("v_max_f32", o, of); run<13>("v_fma_f32", o, of); run<14>("v_cndmask(sgpr)", o, of);
+    run<15>("v_min3_f32", o, of); run<16>("v_max3_f32", o, of); run<17>("v_min_u32", o, of);
+    run<18>("v_cvt_f32_ubyte1", o, of); run<19>("v_pk_fma_f32", o, of); run<20>("v_cmp_f32(vcc)", o, of);
+    run<21>("v_min_f32", o, of); run<22>("v_fma_f32(sgpr)", o, of); run<23>("v_med3_f32", o, of);
+    run<24>("v_cvt_f32_f64", o, of); run<25>("v_mul_f32", o, of);
     return 0;
 }
