@@ -70,13 +70,19 @@ def parse():
     # 2000 C3 frames = ~1.3 s timed at N = 1: long enough for an outside GPU-busy sampler
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--config", default="c3", choices=["c2", "c3", "c5", "c3i", "c3g", "c3d"],
+    p.add_argument("--config", default="c3", choices=["c2", "c3", "c5", "c3i", "c3g", "c3d", "c3r"],
                    help="c3 (default, BASELINE configs[2]); c2 / c5 (configs[1] / [4]); c3i: C3 as 25 mesh "
                         "instances with transforms (literal TLAS->BLAS walk); c3g: C3 with glass spheres and two "
-                        "area lights (full trace() kernels); c3d: the glass spheres with the point light only")
+                        "area lights (full trace() kernels); c3d: the glass spheres with the point light only; c3r: c3g "
+                        "with rough glass (the depth-first k_events pass)")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong (default): one frame per step split over the ranks (C4); "
                         "weak: every rank renders a full frame per step")
+    p.add_argument("--gather", default="shared", choices=["shared", "staged"],
+                   help="N > 1 strong: shared (default) = every rank's kernels store their rows straight into "
+                        "one shared page-locked framebuffer; staged = rows delivered by each GPU's DMA engine "
+                        "into a private page-locked frame, then copied by the rank's host thread into the "
+                        "shared frame (no concurrent PCIe stores from 8 GPUs into one segment)")
     p.add_argument("--in-flight", type=int, default=0,
                    help="renders in flight (rt_render_submit); 1 = one frame at a time; 0 = RT_MAX_IN_FLIGHT (16)")
     p.add_argument("--hw-queues", type=int, default=-1,
@@ -127,9 +133,10 @@ class SharedFrame:
         self._mm = mmap.mmap(self._fh.fileno(), nbytes)
         self.array = np.frombuffer(self._mm, dtype=np.uint8)   # zero-filled by the truncate
 
-    def close(self, dist):
+    def close(self, dist, registered=True):
         import myraytracer_amd as M
-        M.unregister_host(self.array)      # the mapping itself goes with the process
+        if registered:
+            M.unregister_host(self.array)  # the mapping itself goes with the process
         if self.world > 1:
             dist.barrier()
         if self.rank == 0:
@@ -189,6 +196,10 @@ def main():
         scene = scenes.scene_c3_glass(path_dir=args.cache, area_lights=False)
         workload = ("C3d: C3's geometry with 24 glass (dielectric, Beer) spheres, 1 point light, "
                     "1920x1080, 1 spp, maxRecursionDepth 4: level passes + node shading + render_full")
+    elif args.config == "c3r":
+        scene = scenes.scene_c3_glass(path_dir=args.cache, rough=True)
+        workload = ("C3r: C3g with rough glass (roughness 0.05), 1 point + 2 area lights, 1920x1080, 1 spp, "
+                    "maxRecursionDepth 4: depth-first k_events + k_jscan + render_full")
     elif args.config == "c3g":
         scene = scenes.scene_c3_glass(path_dir=args.cache)
         workload = ("C3g: C3's geometry with 24 glass (dielectric, Beer) spheres, 1 point + 2 area lights, "
@@ -212,41 +223,62 @@ def main():
     # per render in flight; frame k goes to framebuffer k mod Q
     Q = max(1, min(args.in_flight, A.RT_MAX_IN_FLIGHT))
     shared = []
+    staged = strong and world > 1 and args.gather == "staged"
+    my_rows = None
     if strong and world > 1:
         for q in range(Q):
             sf = SharedFrame(W * H * 4, rank, world, dist, f"{args.config}{q}")
-            M.register_host(sf.array)
+            if not staged:
+                M.register_host(sf.array)
             shared.append(sf)
-        fbs = [sf.array.reshape(H, W, 4) for sf in shared]
+        gathered = [sf.array.reshape(H, W, 4) for sf in shared]
+        if staged:
+            # private page-locked frames, written by the DMA engine; the host copies this rank's
+            # rows into the shared frame after each wait (8-row chunks c = rank mod world)
+            fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
+            for fb_ in fbs:
+                fb_[:] = 0
+            my_rows = np.concatenate([np.arange(8 * c, min(8 * c + 8, H)) for c in range(first, (H + 7) // 8, step)])
+            eng.set_option("submit_dma", 1)
+        else:
+            fbs = gathered
     else:
         fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
         for fb_ in fbs:
             fb_[:] = 0
+        gathered = fbs
 
     # frames through rt_render_submit / rt_render_wait with Q renders in flight (the reference's
     # render is async, RayTracer.swift:137-205), arguments marshalled once (engine.frame_pipeline)
     submit, wait = eng.frame_pipeline(0, first, step, fbs, frame_layout=True)
+    if my_rows is not None:                           # frame_pipeline rendered every buffer once
+        for q in range(Q):
+            gathered[q][my_rows] = fbs[q][my_rows]
 
     submit_s = [0.0]                                  # host time inside rt_render_submit (timed frames)
+
+    def finish(k, ticket, stats_out):
+        s_ = wait(ticket)
+        if my_rows is not None:                       # staged gather: this rank's rows to the shared frame
+            gathered[k % Q][my_rows] = fbs[k % Q][my_rows]
+        if stats_out is not None:
+            stats_out.append((s_.kernel_ms, s_.milliseconds))
+        return s_
 
     def run(k_frames, stats_out=None):
         pend = collections.deque()
         for k in range(k_frames):
             if len(pend) == Q:
-                s_ = wait(pend.popleft())
-                if stats_out is not None:
-                    stats_out.append((s_.kernel_ms, s_.milliseconds))
+                finish(*pend.popleft(), stats_out)
             if stats_out is not None:
                 ts = time.perf_counter()
-                pend.append(submit(k))
+                pend.append((k, submit(k)))
                 submit_s[0] += time.perf_counter() - ts
             else:
-                pend.append(submit(k))
+                pend.append((k, submit(k)))
         last = None
         while pend:
-            last = wait(pend.popleft())
-            if stats_out is not None:
-                stats_out.append((last.kernel_ms, last.milliseconds))
+            last = finish(*pend.popleft(), stats_out)
         return last
 
     st = run(max(1, args.warmup))
@@ -280,17 +312,38 @@ def main():
     tot = np.array([rays_rank, rays_primary + shadow_cast, shadow_cast, shadow_traced], dtype=np.float64) * args.steps
     per_rank = None
     if world > 1:
+        # the same pipelined loop with the image left in HBM (option submit_dma = 2: rows rendered
+        # into device staging, not delivered): each rank's device-only time per frame, so the first
+        # multi-GPU line tells compute scaling from host-gather bandwidth
+        dma_prev = eng.get_option("submit_dma")
+        eng.set_option("submit_dma", 2)
+        n_dev = max(20, min(args.steps, 200))
+        torch.cuda.synchronize()
+        td = time.perf_counter()
+        saved = my_rows
+        my_rows = None
+        run(n_dev)
+        my_rows = saved
+        torch.cuda.synchronize()
+        dev_ms = (time.perf_counter() - td) * 1e3 / n_dev
+        eng.set_option("submit_dma", dma_prev)
         # every rank's own clock and host submit cost, so an N > 1 line shows its imbalance
-        mine = torch.tensor([t_elapsed * 1e3 / args.steps, submit_s[0] * 1e6 / args.steps, float(rows)],
+        mine = torch.tensor([t_elapsed * 1e3 / args.steps, submit_s[0] * 1e6 / args.steps, float(rows), dev_ms],
                             dtype=torch.float64)
-        allr = [torch.zeros(3, dtype=torch.float64) for _ in range(world)]
+        allr = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(allr, mine)
         ms_r = [round(float(x[0]), 4) for x in allr]
-        per_rank = {"ms_per_step": ms_r, "submit_us_per_frame": [round(float(x[1]), 2) for x in allr],
+        dv_r = [round(float(x[3]), 4) for x in allr]
+        per_rank = {"ms_per_step": ms_r, "device_ms_per_frame": dv_r,
+                    "submit_us_per_frame": [round(float(x[1]), 2) for x in allr],
                     "rows": [int(x[2]) for x in allr], "min_ms": min(ms_r), "max_ms": max(ms_r),
-                    "imbalance": round(max(ms_r) / max(1e-9, min(ms_r)), 4),
-                    "what": "per rank: its own timed-region clock per frame (value uses the max), host time "
-                            "inside rt_render_submit per frame, rows of the frame it renders"}
+                    "device_max_ms": max(dv_r), "delivery_overhead": round(max(ms_r) / max(1e-9, max(dv_r)), 4),
+                    "imbalance": round(max(ms_r) / max(1e-9, min(ms_r)), 4), "gather": args.gather,
+                    "what": "per rank: its own timed-region clock per frame (value uses the max, image delivered "
+                            "to the shared host frame), the same pipelined loop with the image left in HBM "
+                            f"({n_dev} frames, device_ms_per_frame), host time inside rt_render_submit per "
+                            "frame, rows of the frame it renders; delivery_overhead = max delivered / max "
+                            "device-only"}
     if world > 1:
         tt = torch.tensor([t_elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -310,10 +363,11 @@ def main():
         dist.barrier()
     gather = None
     if rank == 0:
-        fb = fbs[(args.steps - 1) % Q]                       # the last frame delivered
-        gather = {"rows_complete": bool(all(np.all(f_[:, :, 3] == 255) for f_ in fbs)),
+        fb = gathered[(args.steps - 1) % Q]                  # the last frame delivered
+        gather = {"rows_complete": bool(all(np.all(f_[:, :, 3] == 255) for f_ in gathered)),
                   "rgba8_sha256": hashlib.sha256(np.ascontiguousarray(fb).tobytes()).hexdigest(),
-                  "frames_identical": bool(all(np.array_equal(f_, fb) for f_ in fbs))}
+                  "frames_identical": bool(all(np.array_equal(f_, fb) for f_ in gathered)),
+                  "mode": args.gather if (strong and world > 1) else "single"}
 
     # ---- roofline (profiles/roofline_<config>.json: PMC passes of this build, tools/pmc_roofline.py)
     roofline = roofline_fields(args, eng, local, first, step, rows, W, kernel_ms, rays_rank, world)
@@ -332,7 +386,7 @@ def main():
             cpu = {"value": None, "unit": "Mrays/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 
     for sf in shared:
-        sf.close(dist)
+        sf.close(dist, registered=not staged)
     if rank == 0:
         line = {
             "metric": "Mrays/s (primary+shadow), 1920x1080 / 1M-tri PLY, at 1/2/4/8 MI355X",
@@ -353,7 +407,10 @@ def main():
                      "value_reference_count": round(float(tot[1] / t_max / 1e6), 2),
                      "note": "value counts shadow rays actually traversed; shadow_cast adds the rays the "
                              "reference casts where N.L <= 0 and discards (value_reference_count)",
-                     "secondary_per_step": int(st.secondary_rays) if world == 1 else None},
+                     "secondary_per_step": int(st.secondary_rays) if world == 1 else None,
+                     "rewalked_per_step": int(getattr(st, "rewalked", 0)),
+                     "rewalked_what": "closest-hit rays of rank 0's share that the four-wide walk handed to the "
+                                      "reference-order walk (two candidates at the final t, wide.h)"},
             "per_rank": per_rank,
             "timing": {"in_flight": Q, "submit_to_done_ms": round(statistics.mean(calls), 4),
                        "submit_us_per_frame": round(submit_s[0] * 1e6 / args.steps, 2),
@@ -394,11 +451,24 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
                              "at a time after the timed steps"}
     if prof is not None and world == 1:
         traffic = prof["hbm_bytes_per_launch"]
-        r["traffic"] = int(traffic)
-        r["achieved"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 2)
-        r["frac"] = round(r["achieved"] / HBM_PEAK_GBS, 4)
         r["traffic_source"] = os.path.relpath(ppath, ROOT)
         r["profile_build_matches"] = prof.get("lib_sha256_16") == lib_sha
+        if r["profile_build_matches"]:
+            # figures from another build's profile would describe that build: only a profile of
+            # this very library fills achieved / frac / traffic
+            r["traffic"] = int(traffic)
+            r["achieved"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 2)
+            r["frac"] = round(r["achieved"] / HBM_PEAK_GBS, 4)
+        if "lane_throughput_frac" in prof and r["profile_build_matches"]:
+            # the resource that binds the kernel: VALU issue.  Every figure from ONE rocprofv3 pass
+            # (tools/pmc_roofline.py --valu): busy = issue cycles / cycles, lane util = active lanes /
+            # 64 per issued instruction, their product = fraction of the SIMDs' lane-cycles used
+            r["compute"] = {
+                "bound": "valu-issue", "valu_busy": prof["valu_busy"], "valu_lane_util": prof["valu_lane_util"],
+                "lane_throughput_frac": prof["lane_throughput_frac"],
+                "valu_insts_per_launch": prof.get("valu_insts_per_launch"),
+                "source": os.path.relpath(ppath, ROOT) + " (valu_pass: GRBM_GUI_ACTIVE, SQ_ACTIVE_INST_VALU, "
+                                                         "SQ_THREAD_CYCLES_VALU of the same dispatches)"}
         r["binding"] = {
             "resource": "VALU issue (FP64 slab/Moeller-Trumbore arithmetic at ~half lane utilisation), with the "
                         "vector-memory data path (TA/TD) next: per-lane BVH record and triangle loads served from L1/L2",
@@ -426,6 +496,9 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
         if r["traffic"] is not None:
             pl["achieved"] = round(r["traffic"] / (ov["union_per_frame_ms"] * 1e-3) / 1e9, 2)
             pl["frac"] = round(pl["achieved"] / HBM_PEAK_GBS, 4)
+        if not pl["profile_build_matches"]:
+            pl.pop("achieved", None)
+            pl.pop("frac", None)
         r["pipelined"] = pl
     r["reference_work"] = {
         "what": "SURVEY.md 8(d) algorithmic bytes of the reference's unpruned walk (56 N_node + 72 N_tri + "

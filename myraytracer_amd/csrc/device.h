@@ -798,7 +798,7 @@ namespace dev {
 // Whole-ray unified walks (identity scenes): closest hit and any hit with one stack.  With a
 // wide tree (RenderParams::wide) and every 1/d in range, the conservative FP32 four-wide walk
 // (wide.h) runs instead; a lane that met two candidates at its final t is re-walked here in
-// the reference's order.  Counting launches keep the binary walk (reference-order tallies).
+// the reference's order.  Reference-order counting launches (count_ref) keep the binary walk.
 template <bool COUNT, bool FAST>
 __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
                                                  double tlo, Hit& h, Stack& st, Counts& c) {
@@ -808,13 +808,13 @@ __device__ __forceinline__ void uni_closest_walk(const RenderParams& P, const V3
         if (COUNT || MYRT_WAVE_TIMES) c.it_closest++;
     } while (unified_step<COUNT, false, FAST>(P, ref, st, o, d, inv, tlo, DINF, h, c) == 0);
 }
-template <bool COUNT>
+template <bool COUNT, bool WIDE = true>
 __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv,
                                             double tlo, Hit& h, Stack& st, Counts& c) {
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
-    if (!COUNT && P.wide && __all(wide_ok(inv))) {
+    if (WIDE && !MYRT_REF(P) && P.wide && __all(wide_ok(inv))) {
         bool tie = false;
-        (void)wide_walk<false>(P, o, d, inv, tlo, DINF, h, tie, st);
+        (void)wide_walk<COUNT, false>(P, o, d, inv, tlo, DINF, h, tie, st, c);
         if (__any(tie) && tie) {                 // equal-t candidates: the reference's order decides
             c.ties++;
             h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
@@ -840,15 +840,15 @@ __device__ __forceinline__ bool uni_occluded_walk(const RenderParams& P, const V
     st.reset(base);
     return r == 2;
 }
-template <bool COUNT>
+template <bool COUNT, bool WIDE = true>
 __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o, const V3& d, double tmax,
                                              Stack& st, Counts& c) {
     if (!P.has_tlas) return false;
     const V3 inv = rcp(d);
-    if (!COUNT && P.wide && __all(wide_ok(inv))) {
+    if (WIDE && !MYRT_REF(P) && P.wide && __all(wide_ok(inv))) {
         Hit hu;
         bool tie = false;
-        return wide_walk<true>(P, o, d, inv, 0.0, tmax, hu, tie, st);
+        return wide_walk<COUNT, true>(P, o, d, inv, 0.0, tmax, hu, tie, st, c);
     }
     if (__all(finite3(inv))) return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
     return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);

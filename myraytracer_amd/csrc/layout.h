@@ -13,6 +13,7 @@
 //   normals : double[9] per TriRec (n0, n1, n2), read only for the final hit.
 //   insts   : DInstance[] (RTContext.swift:43-61) + TLAS leaf instance lists.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace myrt {
@@ -69,13 +70,16 @@ static_assert(sizeof(CTri) == 48, "CTri is 48 B");
 // further per render (RenderParams::wdelta) so a conservative FP32 test passes whenever the
 // reference's FP64 test of any leaf below passes.  Leaf boxes are then checked exactly (FP64,
 // lbox) before a hit is accepted.  Slots [axis][child], SoA per axis.
+// Row a of hi lies 64 B after row a of lo, so a lane reads its near and far rows at byte offsets
+// n and n ^ 64 (wide.h WRay).
 struct alignas(128) W4Node {
     float lo[3][4];       // child c box min along axis a: lo[a][c] (rounded down)
-    float hi[3][4];       // ... max (rounded up); an empty slot has lo = hi = +inf (never hit)
     int32_t ref[4];       // >= 0: W4Node index; < 0: ~first TriRec of a reference leaf run
+    float hi[3][4];       // ... max (rounded up); an empty slot has lo = hi = +inf (never hit)
     int32_t pad[4];
 };
 static_assert(sizeof(W4Node) == 128, "W4Node is one 128-B line");
+static_assert(offsetof(W4Node, hi) == offsetof(W4Node, lo) + 64, "near/far rows 64 B apart");
 
 struct DMaterial {        // ParsingKit Material fields used by trace()
     double ambient[3], diffuse[3], specular[3], mirror[3], absorption[3];

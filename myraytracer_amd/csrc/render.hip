@@ -38,11 +38,11 @@ __device__ __forceinline__ unsigned long long pixel_seed(int i, int j) {
 }
 
 // Closest hit of one ray by the scene's walk (WALK, render_kernel).
-template <bool COUNT, int WALK>
+template <bool COUNT, int WALK, bool WIDE = true>
 __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
                                              double time, Hit& h, Stack& st, Counts& c) {
     if (WALK == kWalkIdentity) {
-        uni_closest<COUNT>(P, o, d, inv, tlo, h, st, c);
+        uni_closest<COUNT, WIDE>(P, o, d, inv, tlo, h, st, c);
     } else if (WALK == kWalkTransformed) {
         h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
         (void)ut_walk<false>(P, o, d, inv, tlo, DINF, time, h, st);
@@ -52,10 +52,10 @@ __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o,
 }
 
 // Any hit of one shadow ray (tMin 0, tMax) by the scene's walk.
-template <bool COUNT, int WALK>
+template <bool COUNT, int WALK, bool WIDE = true>
 __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time,
                                               Stack& st, Counts& c) {
-    if (WALK == kWalkIdentity) return uni_occluded<COUNT>(P, o, d, tmax, st, c);
+    if (WALK == kWalkIdentity) return uni_occluded<COUNT, WIDE>(P, o, d, tmax, st, c);
     if (WALK == kWalkTransformed) {
         if (!P.has_tlas) return false;
         Hit hu;
@@ -68,7 +68,7 @@ __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o
 // terms to Lo.  With !(N.L > 0) the reference discards the occlusion result, so that walk is
 // skipped; the ray is still counted as cast.
 // park/unpark: the caller's PCG32 state moves to LDS around each walk (trace_path BOUNCE).
-template <bool COUNT, int WALK, class Park, class Unpark>
+template <bool COUNT, int WALK, bool WIDE, class Park, class Unpark>
 __device__ __forceinline__ void point_lights(const RenderParams& P, const DMaterial& M, const V3& N, const V3& p,
                                              const V3& d, double time, Stack& st, Counts& c, V3& Lo, Park park,
                                              Unpark unpark) {
@@ -99,7 +99,7 @@ __device__ __forceinline__ void point_lights(const RenderParams& P, const DMater
         if (NdotL > 0 || MYRT_REF(P)) {
             c.shadow_traced++;
             park();
-            const bool blocked = walk_occluded<COUNT, WALK>(P, so, wi, dist, time, st, c);
+            const bool blocked = walk_occluded<COUNT, WALK, WIDE>(P, so, wi, dist, time, st, c);
             unpark();
             if (!blocked && NdotL > 0) Lo = Lo + contrib;
         }
@@ -179,6 +179,12 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, int i, int j,
 // its reflected ray to its pixel's level-1 record (slot `qtile * 64 + lane`, qtile = this wave's
 // tile) and sets `deferred`; k_bounce delivers that pixel.  The PCG32 state is read from
 // rng_slot (the caller parks it there) and (i, j) give its stream.
+// The bounce megakernel (C5's mirror scenes) walks the four-wide tree too, at 4 waves/SIMD
+// (MYRT_BOUNCE_WPE): C5 5020 vs 4733 Mrays/s for the binary walk at 6 waves, which was the binary
+// walk's best occupancy; the wide walk at 5 waves spills (4142), DESIGN.md §4.
+#ifndef MYRT_BOUNCE_WIDE
+#define MYRT_BOUNCE_WIDE 1
+#endif
 template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
                          Counts& c, __attribute__((address_space(3))) double* rng_slot, int i = 0, int j = 0,
@@ -199,7 +205,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         const V3 inv = rcp(d);
         Hit h;
         park();
-        walk_closest<COUNT, WALK>(P, o, d, inv, tlo, time, h, st, c);
+        walk_closest<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE>(P, o, d, inv, tlo, time, h, st, c);
         unpark();
         if (h.inst < 0) { L = ld3(P.background); break; }
         V3 p, Ngeo;
@@ -228,7 +234,8 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 }
             }
         }
-        if (computeDirect) point_lights<COUNT, WALK>(P, M, N, p, d, time, st, c, Lo, park, unpark);
+        if (computeDirect)
+            point_lights<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE>(P, M, N, p, d, time, st, c, Lo, park, unpark);
         if (QUEUE && q >= 0) {
             queue_write_lo(P, q, Lo);
             *deferred = true;
@@ -285,7 +292,7 @@ constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;
 constexpr int kTileW = 8;    // 8x8 pixel tiles (16x4 / 32x2 measured slower: DESIGN.md §4)
 typedef __attribute__((address_space(3))) double lds_f64;
 #ifndef MYRT_BOUNCE_WPE
-#define MYRT_BOUNCE_WPE 6   // the bounce (mirror/conductor) instantiation: 6 waves/SIMD (80 VGPRs; C5 -7.5 %)
+#define MYRT_BOUNCE_WPE 4   // the bounce (mirror/conductor) instantiation: 4 waves/SIMD with the wide walk
 #endif
 #ifndef MYRT_QPRIM_WPE
 #define MYRT_QPRIM_WPE 4    // the queued primary pass of the compacted bounce render
@@ -654,7 +661,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
                     cnt.secondary++;
                 }
                 auto none = []() {};
-                if (computeDirect) point_lights<false, WALK>(P, M, N, p, d, time, st, cnt, Lo, none, none);
+                if (computeDirect) point_lights<false, WALK, true>(P, M, N, p, d, time, st, cnt, Lo, none, none);
                 if (want) {
                     queue_write_lo(P, q, Lo);
                     ends = false;

@@ -613,7 +613,9 @@ static void build_wide(HostScene& S) {
     S.wide_root = B.build(root);
     // a walk holds at most three deferred slots per wide level on its path (plus slack): it must
     // fit the device stack (device.h Stack, kStackCap), else the binary walk
-    if (!std::isfinite(S.wide_coord) || 3 * (int64_t)B.max_depth + 2 > kStackCap) {
+    // (and the walk addresses nodes by 32-bit byte offsets: the array must stay below 4 GB)
+    if (!std::isfinite(S.wide_coord) || 3 * (int64_t)B.max_depth + 2 > kStackCap ||
+        S.wnodes.size() * sizeof(W4Node) >= (size_t(1) << 32)) {
         S.wnodes.clear(); S.lbox.clear(); S.wide_root = -1;
     }
 }

@@ -31,10 +31,15 @@
 namespace myrt {
 namespace dev {
 
+// The ray in the walk's FP32 form.  Per axis the near plane of every box is lo when 1/d >= 0 and
+// hi otherwise: the walk reads each slot's near and far planes directly (a per-lane byte offset
+// into the node, nx/ny/nz) instead of taking min/max of both plane distances - the same values
+// (FMA is monotone, and the lo-plane offset is below the hi-plane one), 24 VALU fewer per node.
 struct WRay {
     float ix, iy, iz;     // 1/d in FP32
-    float lx, ly, lz;     // -(o/d) - wdelta/d: offset of the lo planes
-    float hx, hy, hz;     // -(o/d) + wdelta/d: offset of the hi planes
+    float nox, noy, noz;  // offset of the near planes: -(o/d) - wdelta*|1/d|
+    float fox, foy, foz;  // offset of the far planes:  -(o/d) + wdelta*|1/d|
+    unsigned nx, ny, nz;  // byte offset of the near-plane row of axis a in a W4Node (lo or hi)
 };
 
 // every |1/d| within [2^-100, 2^100] (finite; FP32 products of scene coordinates stay finite)
@@ -47,9 +52,13 @@ __device__ __forceinline__ WRay wide_ray(const RenderParams& P, const V3& o, con
     WRay r;
     r.ix = (float)inv.x; r.iy = (float)inv.y; r.iz = (float)inv.z;
     const double ox = o.x * inv.x, oy = o.y * inv.y, oz = o.z * inv.z;
-    const double dx = P.wdelta * inv.x, dy = P.wdelta * inv.y, dz = P.wdelta * inv.z;
-    r.lx = (float)(-ox - dx); r.ly = (float)(-oy - dy); r.lz = (float)(-oz - dz);
-    r.hx = (float)(-ox + dx); r.hy = (float)(-oy + dy); r.hz = (float)(-oz + dz);
+    const double dx = P.wdelta * fabs(inv.x), dy = P.wdelta * fabs(inv.y), dz = P.wdelta * fabs(inv.z);
+    r.nox = (float)(-ox - dx); r.noy = (float)(-oy - dy); r.noz = (float)(-oz - dz);
+    r.fox = (float)(-ox + dx); r.foy = (float)(-oy + dy); r.foz = (float)(-oz + dz);
+    constexpr unsigned kHi = offsetof(W4Node, hi);        // 64: hi row a = lo row a + 64 B
+    r.nx = (inv.x >= 0 ? 0u : kHi) + 0u * 16u;
+    r.ny = (inv.y >= 0 ? 0u : kHi) + 1u * 16u;
+    r.nz = (inv.z >= 0 ? 0u : kHi) + 2u * 16u;
     return r;
 }
 
@@ -69,18 +78,28 @@ __device__ __forceinline__ unsigned long long wide_entry(int ref, float t) {
 // when no slot is hit (the caller pops).
 template <bool SHADOW>
 __device__ __forceinline__ bool wide_inner(const RenderParams& P, int& ref, const WRay& R, float lim, Stack& st) {
-    const W4Node N = P.wnodes[ref];
+    // near / far plane rows of this lane's direction octant (the far row of axis a is the other of
+    // lo[a] / hi[a], 64 B away: offset n ^ 64)
+    // 32-bit byte offsets from the array base (the host keeps the node array below 4 GB): the loads
+    // take the SGPR-base + VGPR-offset form instead of a 64-bit address add per row
+    const char* base = reinterpret_cast<const char*>(P.wnodes);
+    const unsigned nb = (unsigned)ref * (unsigned)sizeof(W4Node);
+    constexpr unsigned kHi = offsetof(W4Node, hi);
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    auto row = [&](unsigned off) { return *reinterpret_cast<const f4*>(base + (size_t)(nb + off)); };
+    const f4 nx = row(R.nx), fx = row(R.nx ^ kHi);
+    const f4 ny = row(R.ny), fy = row(R.ny ^ kHi);
+    const f4 nz = row(R.nz), fz = row(R.nz ^ kHi);
+    const int4 refs = *reinterpret_cast<const int4*>(base + (size_t)(nb + (unsigned)offsetof(W4Node, ref)));
+    const int nr[4] = {refs.x, refs.y, refs.z, refs.w};
     float a[4];
     bool h[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const float tlx = __builtin_fmaf(N.lo[0][c], R.ix, R.lx), thx = __builtin_fmaf(N.hi[0][c], R.ix, R.hx);
-        const float tly = __builtin_fmaf(N.lo[1][c], R.iy, R.ly), thy = __builtin_fmaf(N.hi[1][c], R.iy, R.hy);
-        const float tlz = __builtin_fmaf(N.lo[2][c], R.iz, R.lz), thz = __builtin_fmaf(N.hi[2][c], R.iz, R.hz);
-        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tlx, thx), __builtin_fminf(tly, thy)),
-                                         __builtin_fminf(tlz, thz));
-        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tlx, thx), __builtin_fmaxf(tly, thy)),
-                                         __builtin_fmaxf(tlz, thz));
+        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nx[c], R.ix, R.nox), __builtin_fmaf(ny[c], R.iy, R.noy)),
+                                         __builtin_fmaf(nz[c], R.iz, R.noz));
+        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaf(fx[c], R.ix, R.fox), __builtin_fmaf(fy[c], R.iy, R.foy)),
+                                         __builtin_fmaf(fz[c], R.iz, R.foz));
         a[c] = tn;
         h[c] = __builtin_fmaxf(tn, P.weps) <= __builtin_fminf(tf, lim);
     }
@@ -88,13 +107,13 @@ __device__ __forceinline__ bool wide_inner(const RenderParams& P, int& ref, cons
     int nref;
     if (SHADOW) {
         n = h[0] ? 0 : h[1] ? 1 : h[2] ? 2 : 3;
-        nref = h[0] ? N.ref[0] : h[1] ? N.ref[1] : h[2] ? N.ref[2] : N.ref[3];
+        nref = h[0] ? nr[0] : h[1] ? nr[1] : h[2] ? nr[2] : nr[3];
     } else {
         const float k0 = h[0] ? a[0] : __builtin_inff(), k1 = h[1] ? a[1] : __builtin_inff();
         const float k2 = h[2] ? a[2] : __builtin_inff(), k3 = h[3] ? a[3] : __builtin_inff();
         const bool p = k1 < k0, q = k3 < k2;
         const float m01 = p ? k1 : k0, m23 = q ? k3 : k2;
-        const int r01 = p ? N.ref[1] : N.ref[0], r23 = q ? N.ref[3] : N.ref[2];
+        const int r01 = p ? nr[1] : nr[0], r23 = q ? nr[3] : nr[2];
         const bool z = m23 < m01;
         nref = z ? r23 : r01;
         n = z ? (q ? 3 : 2) : (p ? 1 : 0);
@@ -109,13 +128,13 @@ __device__ __forceinline__ bool wide_inner(const RenderParams& P, int& ref, cons
         int p = st.sp;
 #pragma unroll
         for (int c = 3; c >= 0; --c) {
-            st.lds[p * Stack::stride] = wide_entry(N.ref[c], a[c]);
+            st.lds[p * Stack::stride] = wide_entry(nr[c], a[c]);
             p += keep[c] ? 1 : 0;
         }
         st.sp = p;
     } else {
 #pragma unroll
-        for (int c = 3; c >= 0; --c) st.push_raw_if(keep[c], wide_entry(N.ref[c], a[c]));
+        for (int c = 3; c >= 0; --c) st.push_raw_if(keep[c], wide_entry(nr[c], a[c]));
     }
     ref = nref;
     return h[0] || h[1] || h[2] || h[3];
@@ -165,9 +184,11 @@ __device__ __forceinline__ int tri_candidate(const Tri& T, const V3& o, const V3
 }
 
 // Closest hit (SHADOW = false: h, tie) or any hit (SHADOW: returns occluded) of one ray.
-template <bool SHADOW>
+// COUNT: the work this walk executes (c.recs = four-wide nodes, c.tris = triangle tests) and its
+// per-iteration divergence (inner step / leaf run), as the binary walk's counters.
+template <bool COUNT, bool SHADOW>
 __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
-                                          double tmax, Hit& h, bool& tie, Stack& st) {
+                                          double tmax, Hit& h, bool& tie, Stack& st, Counts& c) {
     const WRay R = wide_ray(P, o, inv);
     const double eps = P.eps;
     float lim = SHADOW ? wide_limit(P, tmax) : 3.0e38f;
@@ -175,6 +196,17 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
     int ref = P.wide_root;
     bool occ = false;
     for (;;) {
+        if (COUNT) {
+            const bool in = ref >= 0;
+            const unsigned long long bi = __ballot(in), bl = __ballot(!in);
+            const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
+            c.it_wave_inner[SHADOW] += (first && bi) ? 1 : 0;
+            c.it_wave_leaf[SHADOW] += (first && bl) ? 1 : 0;
+            c.it_lane_inner[SHADOW] += in ? 1 : 0;
+            c.it_lane_leaf[SHADOW] += in ? 0 : 1;
+            if (SHADOW) c.it_shadow++; else c.it_closest++;
+            if (in) c.recs++;
+        }
         if (ref >= 0) {
             if (wide_inner<SHADOW>(P, ref, R, lim, st)) continue;
         } else {
@@ -183,6 +215,7 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
             auto run = [&](const auto* tris) {
                 for (int t = t0;; ++t) {
                     const auto T = tris[t];                // by value: `last` arrives with the vertices
+                    if (COUNT) c.tris++;
                     if (SHADOW) {
                         if (tri_shadow(T, o, d, 0.0, tmax, eps, P.fast_rcp)) {
                             if (box == 0) box = leaf_box_exact(P, t0, o, d) ? 1 : 2;

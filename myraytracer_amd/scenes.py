@@ -305,12 +305,15 @@ def scene_c3_instanced(path_dir: str = None, width: int = 1920, height: int = 10
 
 
 def scene_c3_glass(path_dir: str = None, width: int = 1920, height: int = 1080, inline: bool = False,
-                   area_lights: bool = True) -> Scene:
+                   area_lights: bool = True, rough: bool = False) -> Scene:
     """C3's geometry with the 24 spheres made of glass (dielectric with Beer absorption, two
     child rays per bounce, Object+Extension.swift:207-251) and two area lights next to the
     point light (:145-186, the chunk-sequential jitterIndex): the full trace() kernels
     (render_full, k_events + k_jscan).  Terrain and spheres are two meshes, maxRecursionDepth 4.
-    area_lights=False: the point light alone (C3d: dielectric paths without the events passes)."""
+    area_lights=False: the point light alone (C3d: dielectric paths without the events passes).
+    rough=True (C3r): the glass is rough (roughness 0.05, Object+Extension.swift:191-198, 209-216):
+    PCG32 draws inside trace() fix the walk order, so the area-light frame takes the depth-first
+    k_events pass instead of the level passes."""
     seed = 42
     hp, hf = heightfield(512, 100.0, 6.0, seed)
     rng = np.random.RandomState(seed + 1)
@@ -327,7 +330,7 @@ def scene_c3_glass(path_dir: str = None, width: int = 1920, height: int = 1080, 
                  near_distance=1.0, image_resolution=(width, height), image_name="c3g.png")
     mats = [_std_material((0.6, 0.7, 0.5)),
             Material(ambient=(0.0, 0.0, 0.0), diffuse=(0.05, 0.05, 0.05), specular=(0.5, 0.5, 0.5), phong=60.0,
-                     ior=1.5, absorption=(0.02, 0.04, 0.08), type="dielectric")]
+                     ior=1.5, absorption=(0.02, 0.04, 0.08), roughness=0.05 if rough else 0.0, type="dielectric")]
     return Scene(cameras=[cam], materials=mats, objects=[terrain, glass],
                  point_lights=[PointLight((30.0, 40.0, 40.0), (3.0e5, 3.0e5, 3.0e5))],
                  area_lights=[AreaLight(position=(-20.0, 30.0, 10.0), normal=(0.5, -1.0, -0.2), radiance=(900.0, 850.0, 800.0),

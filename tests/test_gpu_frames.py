@@ -197,6 +197,8 @@ def test_bench_strong_split_two_ranks_gathers_the_same_frame():
     common = ["--config", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-side-paths"]
     one = _bench(["--gpus", "1"] + common, {})
     two = _bench(["--gpus", "2"] + common, {"MYRT_BENCH_DEVICE": "0"})
+    two_staged = _bench(["--gpus", "2", "--gather", "staged"] + common, {"MYRT_BENCH_DEVICE": "0"})
+    assert two_staged["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["scaling"] == "strong"
     assert one["gather"]["rows_complete"] and two["gather"]["rows_complete"]
     assert two["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
@@ -220,11 +222,18 @@ def test_bench_strong_split_eight_ranks_on_one_gpu():
     assert eight["rays"]["per_step"] == one["rays"]["per_step"]
     pr = eight["per_rank"]
     assert len(pr["ms_per_step"]) == 8 and pr["max_ms"] >= pr["min_ms"] > 0
+    assert len(pr["device_ms_per_frame"]) == 8 and min(pr["device_ms_per_frame"]) > 0
     assert sum(pr["rows"]) == 600 and all(x > 0 for x in pr["submit_us_per_frame"])
+    # staged gather: each GPU's DMA engine delivers into a private frame, the rank's host thread
+    # copies its rows into the shared frame - the same image
+    staged = _bench(["--gpus", "8", "--gather", "staged"] + common, {"MYRT_BENCH_DEVICE": "0"})
+    assert staged["gather"]["mode"] == "staged" and staged["gather"]["rows_complete"]
+    assert staged["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
+    assert staged["per_rank"]["gather"] == "staged" and len(staged["per_rank"]["device_ms_per_frame"]) == 8
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("name", ["c3i", "c3g", "c3d"])
+@pytest.mark.parametrize("name", ["c3i", "c3g", "c3d", "c3r"])
 def test_general_path_bench_configs_full_frame(scene_dir, name):
     """The bench's general-path configs on full 1920x1080 frames against the oracle: C3i (C3's
     geometry as 25 transformed mesh instances: the literal TLAS->BLAS walk, RTContext.swift:
@@ -233,6 +242,7 @@ def test_general_path_bench_configs_full_frame(scene_dir, name):
     passes + node shading without events), through bench.py's call (RGBA8 into page-locked
     memory) and the FP64 frame."""
     make = {"c3i": scenes.scene_c3_instanced, "c3g": scenes.scene_c3_glass,
+            "c3r": lambda path_dir: scenes.scene_c3_glass(path_dir=path_dir, rough=True),
             "c3d": lambda path_dir: scenes.scene_c3_glass(path_dir=path_dir, area_lights=False)}[name]
     sc = make(path_dir=scene_dir)
     ref, ref8, ost = oracle.OracleScene(_inline(sc)).render(0, threads=0, rgba=True)

@@ -88,15 +88,18 @@ def test_pmc_roofline_summary(tmp_path):
         _write_csv(str(tmp_path / sub / "x/1_counter_collection.csv"), rows)
     pmc("fetch", {"FETCH_SIZE": 87000.0})
     pmc("write", {"WRITE_SIZE": 11000.0})
-    pmc("td", {"GRBM_GUI_ACTIVE": 15_000_000.0, "TD_TD_BUSY_sum": 340_000_000.0, "TA_BUSY_avr": 700_000.0,
-               "SQ_THREAD_CYCLES_VALU": 10_500_000_000.0})
-    pmc("sq", {"SQ_ACTIVE_INST_VALU": 318_000_000.0})
+    pmc("td", {"GRBM_GUI_ACTIVE": 15_000_000.0, "TD_TD_BUSY_sum": 340_000_000.0, "TA_BUSY_avr": 700_000.0})
+    # the compute roofline's own pass: its GRBM_GUI_ACTIVE (not the TD pass's) divides its SQ counters
+    pmc("valu", {"GRBM_GUI_ACTIVE": 16_000_000.0, "SQ_ACTIVE_INST_VALU": 318_000_000.0,
+                 "SQ_THREAD_CYCLES_VALU": 10_500_000_000.0, "SQ_INSTS_VALU": 300_000_000.0})
+    pmc("sq", {"SQ_INSTS_SALU": 1.0})
     lib = tmp_path / "lib.so"
     lib.write_bytes(b"not a library")
     out = tmp_path / "roofline.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_roofline.py"), "--kernel", K,
                     "--trace", str(tmp_path / "trace"), "--fetch", str(tmp_path / "fetch"),
-                    "--write", str(tmp_path / "write"), "--td", str(tmp_path / "td"), "--sq", str(tmp_path / "sq"),
+                    "--write", str(tmp_path / "write"), "--td", str(tmp_path / "td"), "--valu", str(tmp_path / "valu"),
+                    "--sq", str(tmp_path / "sq"),
                     "--lib", str(lib), "-o", str(out)], check=True, capture_output=True)
     r = json.loads(out.read_text())
     assert r["kernel_ms"] == 0.75 and r["trace_calls"] == 45 and r["pmc_launches"] == [3, 3]
@@ -104,6 +107,8 @@ def test_pmc_roofline_summary(tmp_path):
     assert r["hbm_bytes_per_launch"] == int(87000 * 1024 * 2 + 11000 * 1024)
     assert r["hbm_GBs"] == pytest.approx((87000 * 2048 + 11000 * 1024) / 0.75e-3 / 1e9, abs=0.1)
     assert r["td_busy"] == pytest.approx((340e6 / 256) / (15e6 / 8), abs=1e-4)
-    assert r["valu_busy"] == pytest.approx(318e6 / 256 / (15e6 / 8), abs=1e-4)
+    assert r["valu_busy"] == pytest.approx(318e6 / 256 / (16e6 / 8), abs=1e-4)
     assert r["valu_lane_util"] == pytest.approx(10.5e9 / (64 * 318e6), abs=1e-4)
+    assert r["lane_throughput_frac"] == pytest.approx(r["valu_busy"] * r["valu_lane_util"], abs=1e-4)
+    assert r["valu_insts_per_launch"] == 300_000_000
     assert len(r["lib_sha256_16"]) == 16

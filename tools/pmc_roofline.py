@@ -2,7 +2,7 @@
 """Roofline summary of the render megakernel from rocprofv3 passes (one counter group per pass).
 
 usage: pmc_roofline.py --kernel 'render_kernel<false, false, 1, false>' --trace DIR --fetch DIR --write DIR
-                       --td DIR [--sq DIR] --lib myraytracer_amd/libmyrt.so -o profiles/roofline_c3.json
+                       --td DIR --valu DIR [--sq DIR] --lib myraytracer_amd/libmyrt.so -o profiles/roofline_c3.json
 
 Per launch (median over the dispatches of that kernel):
   hbm_bytes_per_launch = FETCH_SIZE x 2 + WRITE_SIZE (KB -> B).  /opt/skills/guides/MI355X_MICROARCH.md,
@@ -11,8 +11,12 @@ Per launch (median over the dispatches of that kernel):
   td_busy  = (TD_TD_BUSY_sum / 256 CUs) / (GRBM_GUI_ACTIVE / 8 XCDs): texture-data (vector-memory
       return) path utilisation - the resource that binds this kernel.
   ta_busy  = TA_BUSY_avr / (GRBM_GUI_ACTIVE / 8).
-  valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)  (needs --sq).
-  valu_busy = SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8)  (rocprofiler-sdk's VALUBusy).
+  The compute roofline, every figure from ONE pass (--valu: GRBM_GUI_ACTIVE, SQ_ACTIVE_INST_VALU,
+  SQ_THREAD_CYCLES_VALU, SQ_INSTS_VALU, ... of the same dispatches):
+  valu_busy = SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8)  (rocprofiler-sdk's VALUBusy),
+  valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU),
+  lane_throughput_frac = valu_busy x valu_lane_util: the fraction of the VALU lane-cycles the
+      kernel's arithmetic used (1.0 = every SIMD issuing full-width every cycle).
   kernel_ms = average duration from the --kernel-trace --stats pass.
 lib_sha256_16 ties the summary to the library build it measured (bench.py checks it).
 """
@@ -59,6 +63,7 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--td", required=True)
+    ap.add_argument("--valu", help="one pass holding GRBM_GUI_ACTIVE + SQ_ACTIVE_INST_VALU + SQ_THREAD_CYCLES_VALU")
     ap.add_argument("--sq")
     ap.add_argument("--lib", required=True)
     ap.add_argument("-o", "--out", required=True)
@@ -76,13 +81,21 @@ def main():
            "hbm_GBs": round((f_kb * 2048 + w_kb * 1024) / (ms * 1e-3) / 1e9, 1),
            "td_busy": round((td / 256) / (gui / 8), 4), "ta_busy": round(ta / (gui / 8), 4),
            "correction": "FETCH_SIZE x2 (gfx950 64-B tally of 128-B requests); MALL hits included"}
-    if a.sq:
-        thr, _ = counter(a.td, "SQ_THREAD_CYCLES_VALU", a.kernel)
-        act, _ = counter(a.sq, "SQ_ACTIVE_INST_VALU", a.kernel)
+    if a.valu:
+        vgui, _ = counter(a.valu, "GRBM_GUI_ACTIVE", a.kernel)
+        thr, _ = counter(a.valu, "SQ_THREAD_CYCLES_VALU", a.kernel)
+        act, _ = counter(a.valu, "SQ_ACTIVE_INST_VALU", a.kernel)
+        ins, _ = counter(a.valu, "SQ_INSTS_VALU", a.kernel)
         res["valu_lane_util"] = round(thr / (64 * act), 4)
         # VALUBusy (rocprofiler-sdk derived counter for gfx950): SQ_ACTIVE_INST_VALU counts
         # quad-cycles per CU summed over its 4 SIMDs -> fraction of cycles the SIMDs issue VALU
-        res["valu_busy"] = round(act / 256 / (gui / 8), 4)
+        res["valu_busy"] = round(act / 256 / (vgui / 8), 4)
+        res["lane_throughput_frac"] = round(res["valu_busy"] * res["valu_lane_util"], 4)
+        res["valu_insts_per_launch"] = int(ins)
+        res["valu_pass"] = {"GRBM_GUI_ACTIVE": vgui, "SQ_ACTIVE_INST_VALU": act, "SQ_THREAD_CYCLES_VALU": thr,
+                            "SQ_INSTS_VALU": ins,
+                            "note": "one rocprofv3 --pmc pass: every compute-roofline figure divides counters "
+                                    "of the same dispatches"}
     with open(a.lib, "rb") as fh:
         res["lib_sha256_16"] = hashlib.sha256(fh.read()).hexdigest()[:16]
     with open(a.out, "w") as fh:

@@ -9,17 +9,18 @@ B="python3 bench.py --steps 20 --warmup 3 --in-flight 1 --no-cpu-baseline --no-s
 case " $* " in
   *" --config c5 "*) K="${KERNEL:-render_kernel<false, true, 1, false>}" ;;
   *" --config c3i "*) K="${KERNEL:-render_kernel<false, false, 2, false>}" ;;
-  *" --config c3g "*) K="${KERNEL:-render_full<false, false, 1>}" ;;
+  *" --config c3g "*|*" --config c3r "*) K="${KERNEL:-render_full<false, false, 1>}" ;;
   *) K="${KERNEL:-render_kernel<false, false, 1, false>}" ;;
 esac
 steps=(
   "${tag}_trace|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_trace -- $B"
   "${tag}_fetch|300|timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_fetch -- $B"
   "${tag}_write|300|timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${tag}_write -- $B"
-  "${tag}_td|300|timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_BUSY_avr TD_TD_BUSY_sum SQ_THREAD_CYCLES_VALU --output-format csv -d gpurun_out/${tag}_td -- $B"
-  "${tag}_sq|300|timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/${tag}_sq -- $B"
+  "${tag}_td|300|timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_BUSY_avr TD_TD_BUSY_sum --output-format csv -d gpurun_out/${tag}_td -- $B"
+  "${tag}_valu|300|timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY --output-format csv -d gpurun_out/${tag}_valu -- $B"
+  "${tag}_sq|300|timeout -s KILL 240 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS --output-format csv -d gpurun_out/${tag}_sq -- $B"
   "${tag}_mix|300|timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM --output-format csv -d gpurun_out/${tag}_mix -- $B"
   "${tag}_ta|300|timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_ADDR_STALLED_BY_TD_CYCLES_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum --output-format csv -d gpurun_out/${tag}_ta -- $B"
-  "${tag}_roofline|60|python3 tools/pmc_roofline.py --kernel '$K' --trace gpurun_out/${tag}_trace --fetch gpurun_out/${tag}_fetch --write gpurun_out/${tag}_write --td gpurun_out/${tag}_td --sq gpurun_out/${tag}_sq --lib myraytracer_amd/libmyrt.so -o gpurun_out/${tag}_roofline.json"
+  "${tag}_roofline|60|python3 tools/pmc_roofline.py --kernel '$K' --trace gpurun_out/${tag}_trace --fetch gpurun_out/${tag}_fetch --write gpurun_out/${tag}_write --td gpurun_out/${tag}_td --valu gpurun_out/${tag}_valu --sq gpurun_out/${tag}_sq --lib myraytracer_amd/libmyrt.so -o gpurun_out/${tag}_roofline.json"
 )
 bash "$(dirname "$0")/gpu_session.sh" "${steps[@]}"
