@@ -40,6 +40,7 @@ struct WRay {
     float nox, noy, noz;  // offset of the near planes: -(o/d) - wdelta*|1/d|
     float fox, foy, foz;  // offset of the far planes:  -(o/d) + wdelta*|1/d|
     unsigned nx, ny, nz;  // byte offset of the near-plane row of axis a in a W4Node (lo or hi)
+    bool uoct;            // every lane of the wave has this direction octant (wave-uniform)
 };
 
 // every |1/d| within [2^-100, 2^100] (finite; FP32 products of scene coordinates stay finite)
@@ -59,6 +60,8 @@ __device__ __forceinline__ WRay wide_ray(const RenderParams& P, const V3& o, con
     r.nx = (inv.x >= 0 ? 0u : kHi) + 0u * 16u;
     r.ny = (inv.y >= 0 ? 0u : kHi) + 1u * 16u;
     r.nz = (inv.z >= 0 ? 0u : kHi) + 2u * 16u;
+    const unsigned oct = r.nx | (r.ny << 8) | (r.nz << 16);
+    r.uoct = __all(oct == (unsigned)__builtin_amdgcn_readfirstlane((int)oct));
     return r;
 }
 
@@ -76,21 +79,59 @@ __device__ __forceinline__ unsigned long long wide_entry(int ref, float t) {
 // hit: continue with the nearest entry, the others are pushed; any hit: continue with the first
 // slot hit (the reference's occludedBLAS takes L first, RTContext.swift:823-825).  Returns false
 // when no slot is hit (the caller pops).
+typedef float wf4 __attribute__((ext_vector_type(4)));
+typedef int wi4 __attribute__((ext_vector_type(4)));
+#ifndef MYRT_WIDE_SCALAR
+#define MYRT_WIDE_SCALAR 1
+#endif
+template <bool SHADOW>
+__device__ __forceinline__ bool wide_node(const RenderParams& P, int& ref, const WRay& R, float lim, Stack& st,
+                                          const wf4& nx, const wf4& fx, const wf4& ny, const wf4& fy, const wf4& nz,
+                                          const wf4& fz, const wi4& refs);
 template <bool SHADOW>
 __device__ __forceinline__ bool wide_inner(const RenderParams& P, int& ref, const WRay& R, float lim, Stack& st) {
     // near / far plane rows of this lane's direction octant (the far row of axis a is the other of
     // lo[a] / hi[a], 64 B away: offset n ^ 64)
+    const char* base = reinterpret_cast<const char*>(P.wnodes);
+    constexpr unsigned kHi = offsetof(W4Node, hi);
+    if (MYRT_WIDE_SCALAR && R.uoct) {
+        // Every lane at the same node with the same octant (the top of the tree for a tile's
+        // coherent rays): the rows come through the scalar cache into SGPRs once for the wave,
+        // instead of 64 copies through the vector-memory data path (TD, ~0.87 busy).
+        const int r0 = __builtin_amdgcn_readfirstlane(ref);
+        if (__all(ref == r0)) {
+            const unsigned long long av = (unsigned long long)(base + (size_t)r0 * sizeof(W4Node));
+            const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
+            const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
+            typedef const __attribute__((address_space(4))) char c4_char;
+            c4_char* sb = (c4_char*)((unsigned long long)alo | ((unsigned long long)ahi << 32));
+            typedef const __attribute__((address_space(4))) wf4 c4_f4;
+            typedef const __attribute__((address_space(4))) wi4 c4_i4;
+            const unsigned ox = __builtin_amdgcn_readfirstlane(R.nx), oy = __builtin_amdgcn_readfirstlane(R.ny),
+                           oz = __builtin_amdgcn_readfirstlane(R.nz);
+            const wf4 nx = *(c4_f4*)(sb + ox), fx = *(c4_f4*)(sb + (ox ^ kHi));
+            const wf4 ny = *(c4_f4*)(sb + oy), fy = *(c4_f4*)(sb + (oy ^ kHi));
+            const wf4 nz = *(c4_f4*)(sb + oz), fz = *(c4_f4*)(sb + (oz ^ kHi));
+            const wi4 refs = *(c4_i4*)(sb + offsetof(W4Node, ref));
+            return wide_node<SHADOW>(P, ref, R, lim, st, nx, fx, ny, fy, nz, fz, refs);
+        }
+    }
     // 32-bit byte offsets from the array base (the host keeps the node array below 4 GB): the loads
     // take the SGPR-base + VGPR-offset form instead of a 64-bit address add per row
-    const char* base = reinterpret_cast<const char*>(P.wnodes);
     const unsigned nb = (unsigned)ref * (unsigned)sizeof(W4Node);
-    constexpr unsigned kHi = offsetof(W4Node, hi);
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    auto row = [&](unsigned off) { return *reinterpret_cast<const f4*>(base + (size_t)(nb + off)); };
-    const f4 nx = row(R.nx), fx = row(R.nx ^ kHi);
-    const f4 ny = row(R.ny), fy = row(R.ny ^ kHi);
-    const f4 nz = row(R.nz), fz = row(R.nz ^ kHi);
-    const int4 refs = *reinterpret_cast<const int4*>(base + (size_t)(nb + (unsigned)offsetof(W4Node, ref)));
+    auto row = [&](unsigned off) { return *reinterpret_cast<const wf4*>(base + (size_t)(nb + off)); };
+    const wf4 nx = row(R.nx), fx = row(R.nx ^ kHi);
+    const wf4 ny = row(R.ny), fy = row(R.ny ^ kHi);
+    const wf4 nz = row(R.nz), fz = row(R.nz ^ kHi);
+    const wi4 refs = *reinterpret_cast<const wi4*>(base + (size_t)(nb + (unsigned)offsetof(W4Node, ref)));
+    return wide_node<SHADOW>(P, ref, R, lim, st, nx, fx, ny, fy, nz, fz, refs);
+}
+
+// The slab tests of one node's four slots and the stack update (wide_inner).
+template <bool SHADOW>
+__device__ __forceinline__ bool wide_node(const RenderParams& P, int& ref, const WRay& R, float lim, Stack& st,
+                                          const wf4& nx, const wf4& fx, const wf4& ny, const wf4& fy, const wf4& nz,
+                                          const wf4& fz, const wi4& refs) {
     const int nr[4] = {refs.x, refs.y, refs.z, refs.w};
     float a[4];
     bool h[4];
