@@ -133,8 +133,11 @@ __device__ __forceinline__ int xcd_tile(int b, int nb, int G) {
 // An entry packs {ref (low 32), high 32 bits of the entry distance (high 32)}: dropping
 // the low mantissa word truncates toward zero, i.e. rounds a positive distance DOWN, so
 // pop-time culling stays conservative (negative distances are never culled).
+// LDS entries per lane: 16 since the four-wide walk (up to three pushes per node; C3 +1.2 %,
+// C5 +1.6 % over 8, profiles/r04g_*).  16 entries + the 4 pixel slots = 10 KB per wave: the
+// 16 waves of a CU at 4 waves/SIMD fill its 160 KB exactly.
 #ifndef MYRT_KLDS
-#define MYRT_KLDS 8
+#define MYRT_KLDS 16
 #endif
 constexpr int kLds = MYRT_KLDS;
 constexpr int kSpill = kStackCap - kLds;   // the host refuses deeper scenes (scene.cpp, RT_ERR_STACK)
@@ -815,7 +818,10 @@ __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, 
     if (WIDE && !MYRT_REF(P) && P.wide && __all(wide_ok(inv))) {
         bool tie = false;
         (void)wide_walk<COUNT, false>(P, o, d, inv, tlo, DINF, h, tie, st, c);
-        if (__any(tie) && tie) {                 // equal-t candidates: the reference's order decides
+#ifndef MYRT_REWALK
+#define MYRT_REWALK 1
+#endif
+        if (MYRT_REWALK && __any(tie) && tie) {  // equal-t candidates: the reference's order decides
             c.ties++;
             h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
             uni_closest_walk<COUNT, true>(P, o, d, inv, tlo, h, st, c);
