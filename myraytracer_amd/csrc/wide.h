@@ -79,6 +79,9 @@ __device__ __forceinline__ unsigned long long wide_entry(int ref, float t) {
 // hit: continue with the nearest entry, the others are pushed; any hit: continue with the first
 // slot hit (the reference's occludedBLAS takes L first, RTContext.swift:823-825).  Returns false
 // when no slot is hit (the caller pops).
+#ifndef MYRT_MT_TWICE
+#define MYRT_MT_TWICE 0
+#endif
 typedef float wf4 __attribute__((ext_vector_type(4)));
 typedef int wi4 __attribute__((ext_vector_type(4)));
 #ifndef MYRT_WIDE_SCALAR
@@ -258,12 +261,27 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
                     const auto T = tris[t];                // by value: `last` arrives with the vertices
                     if (COUNT) c.tris++;
                     if (SHADOW) {
+#if MYRT_MT_TWICE   // measurement variant: every triangle test runs twice (the difference prices the tests)
+                        {
+                            V3 o2 = o;
+                            asm volatile("" : "+v"(o2.x));
+                            if (tri_shadow(T, o2, d, 0.0, tmax, eps, P.fast_rcp)) asm volatile("" ::: "memory");
+                        }
+#endif
                         if (tri_shadow(T, o, d, 0.0, tmax, eps, P.fast_rcp)) {
                             if (box == 0) box = leaf_box_exact(P, t0, o, d) ? 1 : 2;
                             if (box == 1) return true;
                         }
                     } else {
                         double tt, uu, vv;
+#if MYRT_MT_TWICE
+                        {
+                            V3 o2 = o;
+                            asm volatile("" : "+v"(o2.x));
+                            double t2, u2, v2;
+                            if (tri_candidate(T, o2, d, tlo, eps, h.t, t2, u2, v2, P.fast_rcp)) asm volatile("" ::: "memory");
+                        }
+#endif
                         const int r = tri_candidate(T, o, d, tlo, eps, h.t, tt, uu, vv, P.fast_rcp);
                         if (r != 0) {
                             if (box == 0) box = leaf_box_exact(P, t0, o, d) ? 1 : 2;
