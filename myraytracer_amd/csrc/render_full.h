@@ -401,8 +401,11 @@ __device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int
 }
 
 // Pass 1: area-light evaluations per pixel of the selection (packed rows).
+// waves/SIMD for the full trace() passes (k_events, k_level, k_shade, render_full; 0 = the compiler's
+// choice, 3 for k_level / k_shade at 138-150 VGPRs).  4 since the four-wide walk: C3g 4.22 -> 3.92,
+// C3d 2.97 -> 2.90, C3r 4.96 -> 4.57 ms per frame pipelined (profiles/r04k_*).
 #ifndef MYRT_FULL_WPE
-#define MYRT_FULL_WPE 0      // waves/SIMD for render_full and k_events (0 = the compiler's choice)
+#define MYRT_FULL_WPE 4
 #endif
 #if MYRT_FULL_WPE > 0
 #define MYRT_FULL_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_FULL_WPE)))
