@@ -147,6 +147,38 @@ __device__ __forceinline__ bool wide_node(const RenderParams& P, int& ref, const
         a[c] = tn;
         h[c] = __builtin_fmaxf(tn, P.weps) <= __builtin_fminf(tf, lim);
     }
+#ifndef MYRT_WIDE_SORT
+#define MYRT_WIDE_SORT 0
+#endif
+    if (!SHADOW && MYRT_WIDE_SORT) {
+        // closest hit, full front-to-back order: sort the four (entry, ref) pairs (5 compare-
+        // exchanges), continue with the nearest, push the others far to near
+        float k[4];
+        int r[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { k[c] = h[c] ? a[c] : __builtin_inff(); r[c] = nr[c]; }
+        auto ce = [&](int i, int j) {
+            const bool sw = k[j] < k[i];
+            const float ki = sw ? k[j] : k[i], kj = sw ? k[i] : k[j];
+            const int ri = sw ? r[j] : r[i], rj = sw ? r[i] : r[j];
+            k[i] = ki; k[j] = kj; r[i] = ri; r[j] = rj;
+        };
+        ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+        if (!__any(st.sp > kLds - 4)) {
+            int p = st.sp;
+#pragma unroll
+            for (int c = 3; c >= 1; --c) {
+                st.lds[p * Stack::stride] = wide_entry(r[c], k[c]);
+                p += k[c] < __builtin_inff() ? 1 : 0;
+            }
+            st.sp = p;
+        } else {
+#pragma unroll
+            for (int c = 3; c >= 1; --c) st.push_raw_if(k[c] < __builtin_inff(), wide_entry(r[c], k[c]));
+        }
+        ref = r[0];
+        return k[0] < __builtin_inff();
+    }
     int n;          // the slot the walk continues with
     int nref;
     if (SHADOW) {
