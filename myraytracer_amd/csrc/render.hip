@@ -170,15 +170,32 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, int i, int j,
     }
 }
 
+constexpr int kPixSlots = 4;   // per lane: pixel sum x/y/z and the parked PCG32 state, after the stacks
+constexpr int kTileW = 8;      // 8x8 pixel tiles (16x4 / 32x2 measured slower: DESIGN.md §4)
+typedef __attribute__((address_space(3))) double lds_f64;
+// This lane's index in its (one-wave) block, computed afresh: the empty asm keeps the compiler from
+// reusing an earlier value, which it would otherwise keep live - spilled - across the walks.
+__device__ __forceinline__ int pix_lane() {
+    int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(l));
+    return l;
+}
+// this lane's pixel slot k (0-2 pixel sum, 3 PCG32 state) of the megakernel's LDS: the [kLds][64]
+// stack slab of the block's one wave, then [kPixSlots][64] doubles
+__device__ __forceinline__ lds_f64* pix_slot(int k) {
+    extern __shared__ unsigned long long lds_stack[];
+    return (lds_f64*)(lds_u64*)(lds_stack + 64 * kLds) + k * 64 + pix_lane();
+}
+
 // trace() (Object+Extension.swift:96-283) for diffuse/mirror/conductor materials and
 // point lights.  The recursion Lo + M*trace(depth+1) is run forward and combined
 // backward with the same per-level NaN guard, so the result is the recursive one.
-// `rng_slot`: this lane's LDS slot for the PCG32 state (BOUNCE: the state waits there while
-// the rays are traced instead of being live - spilled - across the walks; nullptr = keep it)
+// `park_rng`: the PCG32 state waits in this lane's LDS pixel slot 3 while the rays are traced
+// (BOUNCE) instead of being live - spilled - across the walks
 // QUEUE (primary pass of the compacted bounce render, !BOUNCE): a mirror/conductor hit writes
 // its reflected ray to its pixel's level-1 record (slot `qtile * 64 + lane`, qtile = this wave's
 // tile) and sets `deferred`; k_bounce delivers that pixel.  The PCG32 state is read from
-// rng_slot (the caller parks it there) and (i, j) give its stream.
+// pixel slot 3 (the caller parks it there) and (i, j) give its stream.
 // The bounce megakernel (C5's mirror scenes) walks the four-wide tree too, at 4 waves/SIMD
 // (MYRT_BOUNCE_WPE): C5 5020 vs 4733 Mrays/s for the binary walk at 6 waves, which was the binary
 // walk's best occupancy; the wide walk at 5 waves spills (4142), DESIGN.md §4.
@@ -187,14 +204,14 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, int i, int j,
 #endif
 template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
-                         Counts& c, __attribute__((address_space(3))) double* rng_slot, int i = 0, int j = 0,
+                         Counts& c, bool park_rng, int i = 0, int j = 0,
                          bool* deferred = nullptr, int qtile = 0) {
     static_assert(!(QUEUE && BOUNCE), "the queued primary pass has no bounce loop");
-    auto park = [&]() { if (BOUNCE && rng_slot) *rng_slot = __builtin_bit_cast(double, rng.state); };
+    auto park = [&]() { if (BOUNCE && park_rng) *pix_slot(3) = __builtin_bit_cast(double, rng.state); };
     auto unpark = [&]() {
-        if (BOUNCE && rng_slot) {
+        if (BOUNCE && park_rng) {
             asm volatile("" ::: "memory");
-            rng.state = __builtin_bit_cast(unsigned long long, (double)*rng_slot);
+            rng.state = __builtin_bit_cast(unsigned long long, (double)*pix_slot(3));
         }
     };
     V3 Lst[BOUNCE ? kMaxDepthGPU : 1], Mst[BOUNCE ? kMaxDepthGPU : 1];
@@ -227,7 +244,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                 if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) P.bmask[qtile] = m;
                 if (want) {
                     q = (long long)qtile * 64 + (threadIdx.x & 63);
-                    PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*rng_slot),
+                    PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*pix_slot(3)),
                                             pixel_seed(i, j));
                     queue_write(P, q, M, d, N, p, r, time, i, j);
                     c.secondary++;
@@ -285,12 +302,6 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 #ifndef MYRT_MEGA_WPE
 #define MYRT_MEGA_WPE 4      // amdgpu_waves_per_eu for the megakernel (0 = compiler default = 2 waves at ~200 VGPRs)
 #endif
-#ifndef MYRT_PIXLDS
-#define MYRT_PIXLDS 1        // pixel sum + PCG32 state kept in LDS across the walks (not spilled)
-#endif
-constexpr int kPixSlots = MYRT_PIXLDS ? 4 : 0;
-constexpr int kTileW = 8;    // 8x8 pixel tiles (16x4 / 32x2 measured slower: DESIGN.md §4)
-typedef __attribute__((address_space(3))) double lds_f64;
 #ifndef MYRT_BOUNCE_WPE
 #define MYRT_BOUNCE_WPE 4   // the bounce (mirror/conductor) instantiation: 4 waves/SIMD with the wide walk
 #endif
@@ -315,126 +326,118 @@ namespace dev {
 // mirror/conductor hits queue their reflected rays and their pixels are stored by k_bounce.
 template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams P) {
-    static_assert(!QUEUE || MYRT_PIXLDS, "the queued primary pass reads the PCG32 state from its LDS slot");
     extern __shared__ unsigned long long lds_stack[];
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
 #if MYRT_WAVE_TIMES
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    // one tile = (TW x waves-per-block) x TH pixels of one selected chunk (one TW x TH
-    // rectangle per wave, TW = kTileW); tiles are row-major over (slot, band, column)
-    constexpr int TW = kTileW, TH = 64 / kTileW, BANDS = 8 / TH;
-    const int wpb = (int)(blockDim.x >> 6);
-    const int gx = (P.cam.width + TW * wpb - 1) / (TW * wpb);
+    // One wave per block (kRenderBlock = 64) renders one kTileW x 8 tile of one selected chunk;
+    // tiles are row-major over (slot in the chunk list, column).  Everything but the lane is
+    // wave-uniform: the lane's pixel is (lane % kTileW, lane / kTileW) in the tile, and it is
+    // recomputed from a fresh lane id where it is needed after the walks (pix_lane), not kept
+    // live - spilled - across them.
+    const int gx = (P.cam.width + kTileW - 1) / kTileW;
     const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
-    const int i = (tile % gx) * (TW * wpb) + wave * TW + (lane % TW);
-    const int slot = tile / (gx * BANDS);              // position in the selected chunk list
-    const int chunk = P.chunk_first + slot * P.chunk_step;
-    const int rowInChunk = ((tile / gx) % BANDS) * TH + lane / TW;
-    const int j = chunk * 8 + rowInChunk;
+    const int chunk = P.chunk_first + (tile / gx) * P.chunk_step;     // slot = tile / gx
+    // the tile's corner in VGPRs: the kernel's SGPRs are at the 106 limit, and uniform values
+    // live across the walks there are spilled to VGPR lanes and restored with v_readlane
+    int i0 = (tile % gx) * kTileW, j0 = chunk * 8;
+    asm volatile("" : "+v"(i0), "+v"(j0));
     const DCamera& C = P.cam;
-    const bool valid = (i < C.width) && (j < C.height);
     Counts cnt{};
-#if MYRT_PIXLDS
-    // this wave's [kPixSlots][64] slab after the stacks
-    lds_f64* pacc = (lds_f64*)(lds_u64*)(lds_stack + (size_t)blockDim.x * kLds) + wave * (kPixSlots * 64) + lane;
-#endif
+    bool valid;
+    {
+        const int lane = pix_lane();
+        valid = (i0 + lane % kTileW < C.width) && (j0 + lane / kTileW < C.height);
+    }
     if (valid) {
         MYRT_STACK(st, lds_stack);
         st.uni_spill = !BOUNCE;     // the LDS-only fast path raised the bounce kernel's spills
-        PCG32 rng(pixel_seed(i, j));
-        V3 pixel = v3(0, 0, 0);
+        const int l0 = pix_lane();
+        PCG32 rng(pixel_seed(i0 + l0 % kTileW, j0 + l0 / kTileW));
         const V3 eye = ld3(C.eye), u = ld3(C.u), v = ld3(C.v), w = ld3(C.w), q00 = ld3(C.q00);
         const int n = C.n;
-        int sampleIndex = 0;
+        // the reference's sy / sx loops (Object+Extension.swift:298-354): sample s is (sx, sy) =
+        // (s % n, s / n), up to C.samples
+        const int ns = min(C.samples, n * n);
         bool deferred = false;
-        for (int sy = 0; sy < n && sampleIndex < C.samples; ++sy) {
-            for (int sx = 0; sx < n; ++sx) {
-                const double xi1 = rng.nextFloat();
-                const double xi2 = rng.nextFloat();
-                const double iOffset = ((double)sx + xi1) / (double)n;
-                const double jOffset = ((double)sy + xi2) / (double)n;
-#if MYRT_PIXLDS
-                // per-sample copies the compiler cannot hoist: otherwise (double)i, (double)j and
-                // eye - w*nd are computed once before the sample loop and spilled across the walks
-                int ii = i, jj = j;
-                double nd = C.nd;
-                asm volatile("" : "+v"(ii), "+v"(jj), "+v"(nd));
-#else
-                const int ii = i, jj = j;
-                const double nd = C.nd;
-#endif
-                const double currentI = (double)ii + iOffset;
-                const double currentJ = (double)jj + jOffset;
-                const V3 vOff = v * (currentJ * C.dv);
-                const V3 rowTopLeft = q00 - vOff;
-                const V3 uOff = u * (currentI * C.du);
-                const V3 s = rowTopLeft + uOff;
-                const V3 dir0 = normalize(s - eye);
-                V3 dir = dir0, camEye = eye;
-                if (C.aperture > 0 && C.focus > 0) {                  // DOF (:325-338)
-                    const V3 forward = -w;
-                    const double denom = dot(dir0, forward);
-                    const double tFocus = fabs(denom) < 1e-6 ? C.focus : (C.focus / denom);
-                    const V3 pFocus = eye + dir0 * tFocus;
-                    const double uRand = rng.nextFloat() - 0.5;
-                    const double vRand = rng.nextFloat() - 0.5;
-                    const V3 lensOffset = ((uRand * u) + (vRand * v)) * C.aperture;
-                    const V3 a = eye + lensOffset;
-                    dir = normalize(pFocus - a);
-                    camEye = a;
-                }
-                const double time = rng.nextFloat();
-                const double denom = dot(dir, w);
-                const double tImg = dot((eye - w * nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
-                const double tlo = smax(tImg, 0.0);
-#if MYRT_PIXLDS
-                // The pixel sum and (when the walk does not draw from it) the PCG32 state wait
-                // in LDS while the rays are traced, so they are not live - spilled - across the
-                // walks; the memory clobber makes the reloads real loads.
-                if (!BOUNCE) pacc[3 * 64] = __builtin_bit_cast(double, rng.state);
-                const V3 col = trace_path<COUNT, BOUNCE, WALK, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt,
-                                                                     pacc + 3 * 64, i, j, &deferred,
-                                                                     tile * wpb + wave);
-                asm volatile("" ::: "memory");
-                if (!BOUNCE) {
-                    rng.state = __builtin_bit_cast(unsigned long long, (double)pacc[3 * 64]);
-                    rng.inc = (pixel_seed(i, j) << 1) | 1ull;     // PCG32(seed) sets inc = seed<<1 | 1
-                }
-                if (sampleIndex == 0) {
-                    pacc[0] = 0.0 + col.x; pacc[64] = 0.0 + col.y; pacc[128] = 0.0 + col.z;
-                } else {
-                    pacc[0] = pacc[0] + col.x; pacc[64] = pacc[64] + col.y; pacc[128] = pacc[128] + col.z;
-                }
-#else
-                const V3 col = trace_path<COUNT, BOUNCE, WALK>(P, camEye, dir, tlo, time, rng, st, cnt, nullptr);
-                pixel = pixel + col;
-#endif
-                sampleIndex += 1;
-                if (sampleIndex >= C.samples) break;
+        // (one flattened loop over s measured 3.5 % slower on C3: profiles/r04q_ab_flat.txt)
+        int s = 0;
+        for (int sy = 0; sy < n && s < ns; ++sy)
+        for (int sx = 0; sx < n && s < ns; ++sx, ++s) {
+            const double xi1 = rng.nextFloat();
+            const double xi2 = rng.nextFloat();
+            const double iOffset = ((double)sx + xi1) / (double)n;
+            const double jOffset = ((double)sy + xi2) / (double)n;
+            // per-sample values the compiler cannot hoist: otherwise (double)i, (double)j and
+            // eye - w*nd are computed once before the sample loop and spilled across the walks
+            const int lane = pix_lane();
+            const int ii = i0 + lane % kTileW, jj = j0 + lane / kTileW;
+            double nd = C.nd;
+            asm volatile("" : "+v"(nd));
+            const double currentI = (double)ii + iOffset;
+            const double currentJ = (double)jj + jOffset;
+            const V3 vOff = v * (currentJ * C.dv);
+            const V3 rowTopLeft = q00 - vOff;
+            const V3 uOff = u * (currentI * C.du);
+            const V3 sp = rowTopLeft + uOff;
+            const V3 dir0 = normalize(sp - eye);
+            V3 dir = dir0, camEye = eye;
+            if (C.aperture > 0 && C.focus > 0) {                  // DOF (:325-338)
+                const V3 forward = -w;
+                const double denom = dot(dir0, forward);
+                const double tFocus = fabs(denom) < 1e-6 ? C.focus : (C.focus / denom);
+                const V3 pFocus = eye + dir0 * tFocus;
+                const double uRand = rng.nextFloat() - 0.5;
+                const double vRand = rng.nextFloat() - 0.5;
+                const V3 lensOffset = ((uRand * u) + (vRand * v)) * C.aperture;
+                const V3 a = eye + lensOffset;
+                dir = normalize(pFocus - a);
+                camEye = a;
+            }
+            const double time = rng.nextFloat();
+            const double denom = dot(dir, w);
+            const double tImg = dot((eye - w * nd) - camEye, w) / (denom == 0.0 ? 4.9406564584124654e-324 : denom);
+            const double tlo = smax(tImg, 0.0);
+            // The pixel sum and (when the walk does not draw from it) the PCG32 state wait in the
+            // wave's LDS pixel slots while the rays are traced, so they are not live - spilled -
+            // across the walks; the memory clobber makes the reloads real loads.
+            if (!BOUNCE) *pix_slot(3) = __builtin_bit_cast(double, rng.state);
+            const V3 col = trace_path<COUNT, BOUNCE, WALK, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt, true,
+                                                                 ii, jj, &deferred, tile);
+            asm volatile("" ::: "memory");
+            if (!BOUNCE) {
+                const int l2 = pix_lane();
+                rng.state = __builtin_bit_cast(unsigned long long, (double)*pix_slot(3));
+                rng.inc = (pixel_seed(i0 + l2 % kTileW, j0 + l2 / kTileW) << 1) | 1ull;   // PCG32(seed): inc = seed<<1 | 1
+            }
+            lds_f64* pacc = pix_slot(0);
+            if (s == 0) {
+                pacc[0] = 0.0 + col.x; pacc[64] = 0.0 + col.y; pacc[128] = 0.0 + col.z;
+            } else {
+                pacc[0] = pacc[0] + col.x; pacc[64] = pacc[64] + col.y; pacc[128] = pacc[128] + col.z;
             }
         }
-#if MYRT_PIXLDS
-        pixel = v3(pacc[0], pacc[64], pacc[128]);
-#endif
+        const lds_f64* pacc = pix_slot(0);
+        const V3 pixel = ns > 0 ? v3(pacc[0], pacc[64], pacc[128]) : v3(0, 0, 0);
         const V3 px = pixel / (double)C.samples;
-        if (!(QUEUE && deferred)) store_pixel(P, i, j, px);          // RayTracer.swift:186-195
+        const int lane = pix_lane();
+        if (!(QUEUE && deferred)) store_pixel(P, i0 + lane % kTileW, j0 + lane / kTileW, px);   // RayTracer.swift:186-195
 #if MYRT_WAVE_TIMES >= 2
-        const size_t o = out_row_of(P, chunk, rowInChunk) * (size_t)C.width + i;
+        const size_t o = out_row_of(P, chunk, lane / kTileW) * (size_t)C.width + i0 + lane % kTileW;
         if (P.wave_times && P.out_rgb) {        // debug: per-lane walk iterations instead of the colour
             P.out_rgb[o * 3 + 0] = (double)cnt.it_closest;
             P.out_rgb[o * 3 + 1] = (double)cnt.it_shadow;
         }
 #endif
     }
+    const int lane = pix_lane();
 #if MYRT_WAVE_TIMES
     if (P.wave_times) {                                              // debug timeline
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         // the wave's walk iterations: its longest lane's, closest hit and any hit
         const unsigned long long mc = wave_max(cnt.it_closest), ms = wave_max(cnt.it_shadow);
         if (lane == 0) {
-            unsigned long long* w = P.wave_times + 3 * ((size_t)blockIdx.x * wpb + wave);
+            unsigned long long* w = P.wave_times + 3 * (size_t)blockIdx.x;
             w[0] = t_start; w[1] = t_end;
             w[2] = (unsigned long long)tile | (std::min(mc, 0xFFFFFull) << 24) | (std::min(ms, 0xFFFFFull) << 44);
         }

@@ -92,10 +92,10 @@ __device__ __forceinline__ bool wide_node(const RenderParams& P, int& ref, const
                                           const wf4& nx, const wf4& fx, const wf4& ny, const wf4& fy, const wf4& nz,
                                           const wf4& fz, const wi4& refs);
 template <bool SHADOW>
-__device__ __forceinline__ bool wide_inner(const RenderParams& P, int& ref, const WRay& R, float lim, Stack& st) {
+__device__ __forceinline__ bool wide_inner(const RenderParams& P, const char* base, int& ref, const WRay& R, float lim,
+                                           Stack& st) {
     // near / far plane rows of this lane's direction octant (the far row of axis a is the other of
-    // lo[a] / hi[a], 64 B away: offset n ^ 64)
-    const char* base = reinterpret_cast<const char*>(P.wnodes);
+    // lo[a] / hi[a], 64 B away: offset n ^ 64); base = P.wnodes
     constexpr unsigned kHi = offsetof(W4Node, hi);
     if (MYRT_WIDE_SCALAR && R.uoct) {
         // Every lane at the same node with the same octant (the top of the tree for a tile's
@@ -148,11 +148,12 @@ __device__ __forceinline__ bool wide_node(const RenderParams& P, int& ref, const
         h[c] = __builtin_fmaxf(tn, P.weps) <= __builtin_fminf(tf, lim);
     }
 #ifndef MYRT_WIDE_SORT
-#define MYRT_WIDE_SORT 0
+#define MYRT_WIDE_SORT 1
 #endif
-    if (!SHADOW && MYRT_WIDE_SORT) {
-        // closest hit, full front-to-back order: sort the four (entry, ref) pairs (5 compare-
-        // exchanges), continue with the nearest, push the others far to near
+    if ((!SHADOW && MYRT_WIDE_SORT) || (SHADOW && MYRT_WIDE_SORT >= 2)) {
+        // closest hit (and, at MYRT_WIDE_SORT 2, any hit), full front-to-back order: sort the four
+        // (entry, ref) pairs (5 compare-exchanges), continue with the nearest, push the others far
+        // to near
         float k[4];
         int r[4];
 #pragma unroll
@@ -271,6 +272,9 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
     const int base = st.sp;
     int ref = P.wide_root;
     bool occ = false;
+    const char* wbase = reinterpret_cast<const char*>(P.wnodes);
+    const auto* ctris = P.ctris;
+    const auto* tris = P.tris;
     for (;;) {
         if (COUNT) {
             const bool in = ref >= 0;
@@ -284,7 +288,7 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
             if (in) c.recs++;
         }
         if (ref >= 0) {
-            if (wide_inner<SHADOW>(P, ref, R, lim, st)) continue;
+            if (wide_inner<SHADOW>(P, wbase, ref, R, lim, st)) continue;
         } else {
             const int t0 = ~ref;
             int box = 0;                                   // leaf box: 0 unchecked, 1 passes, 2 fails
@@ -332,7 +336,7 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
                 }
                 return false;
             };
-            if (P.ctris ? run(P.ctris) : run(P.tris)) { occ = true; break; }
+            if (ctris ? run(ctris) : run(tris)) { occ = true; break; }
         }
         if (!wide_pop(st, base, lim, ref)) break;
     }

@@ -1,10 +1,13 @@
 #!/usr/bin/env bash
 # The round's final measurement session (run on the GPU box via gpurun): PMC + kernel-trace
 # profiles of C3/C5 (tools/prof_session.sh), the bench loop's kernel overlap
-# (tools/overlap_session.sh), smoke, bench lines of every config and the GPU suite.
-# usage: gpurun -- 'bash tools/final_session.sh'  ->  gpurun_out/r03w_*
+# (tools/overlap_session.sh), a one-pass VALU PMC of the full trace() frames (C3g, C3r), smoke,
+# bench lines of every config and the GPU suite.
+# usage: gpurun -- 'bash tools/final_session.sh TAG'  ->  gpurun_out/TAG_*
 set -u
-T=r03w
+T="${1:-r04z}"
+G="python3 bench.py --steps 10 --warmup 2 --in-flight 1 --no-cpu-baseline --no-side-paths"
+VALU="GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY"
 bash tools/prof_session.sh ${T}_c3 || exit $?
 bash tools/prof_session.sh ${T}_c5 --config c5 || exit $?
 bash tools/overlap_session.sh ${T}_c3 c3 300 || exit $?
@@ -14,8 +17,12 @@ bash tools/gpu_session.sh \
  "${T}_bc3|300|python3 bench.py > gpurun_out/${T}_bench_c3.json" \
  "${T}_bc5|300|python3 bench.py --config c5 --steps 400 --warmup 20 --no-cpu-baseline > gpurun_out/${T}_bench_c5.json" \
  "${T}_bc3i|300|python3 bench.py --config c3i --steps 400 --warmup 20 --no-cpu-baseline > gpurun_out/${T}_bench_c3i.json" \
- "${T}_bc3g|300|python3 bench.py --config c3g --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_bench_c3g.json" \
- "${T}_bc3g_trace|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_c3g_trace -- python3 bench.py --config c3g --steps 10 --warmup 2 --in-flight 1 --no-cpu-baseline --no-side-paths"
+ "${T}_bc3g|300|python3 bench.py --config c3g --steps 60 --warmup 5 --no-cpu-baseline > gpurun_out/${T}_bench_c3g.json" \
+ "${T}_bc3r|300|python3 bench.py --config c3r --steps 60 --warmup 5 --no-cpu-baseline > gpurun_out/${T}_bench_c3r.json" \
+ "${T}_bc3d|300|python3 bench.py --config c3d --steps 60 --warmup 5 --no-cpu-baseline > gpurun_out/${T}_bench_c3d.json" \
+ "${T}_c3g_trace|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_c3g_trace -- $G --config c3g" \
+ "${T}_c3r_trace|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_c3r_trace -- $G --config c3r" \
+ "${T}_c3g_valu|300|timeout -s KILL 240 rocprofv3 --pmc $VALU --output-format csv -d gpurun_out/${T}_c3g_valu -- $G --config c3g" \
+ "${T}_c3r_valu|300|timeout -s KILL 240 rocprofv3 --pmc $VALU --output-format csv -d gpurun_out/${T}_c3r_valu -- $G --config c3r" || exit $?
 bash tools/gpu_session.sh \
- "${T}_bc3d|300|python3 bench.py --config c3d --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_bench_c3d.json" \
  "${T}_suite|700|python -u -m pytest -x -v --timeout 400 --timeout-method thread tests -m gpu"
