@@ -88,6 +88,8 @@ def parse():
     p.add_argument("--hw-queues", type=int, default=-1,
                    help="GPU_MAX_HW_QUEUES for this process (-1 = 32: one per render in flight and the "
                         "library's own streams; 0 = HIP's default)")
+    p.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                   help="render option for the run (rt_scene_set_option, INTEGRATION.md table); repeatable")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-side-paths", action="store_true", help="skip the fp64 / device-only side measurements")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share (OMP_NUM_THREADS / affinity)")
@@ -208,6 +210,11 @@ def main():
         scene = scenes.scene_c5(path_dir=args.cache)
         workload = "C5: ~10M-tri (2 meshes, mirror spheres), 3840x2160, depth-4 reflections"
     eng = M.RayTracerEngine(scene, devices=[local])
+    options = {}
+    for o in args.option:
+        name, _, value = o.partition("=")
+        eng.set_option(name, int(value))
+        options[name] = int(value)
     info = eng.info()
     log(f"[rank {rank}] scene ready in {time.time() - t0:.1f}s: tris={info.triangles} recs={info.blas_nodes} "
         f"build={info.build_ms:.0f}ms upload={info.upload_ms:.0f}ms dev={info.device_bytes / 1e6:.0f}MB")
@@ -400,7 +407,8 @@ def main():
                                      "rows stored into shared page-locked framebuffers" if strong else
                                      f"one full frame per GPU per step, {world} GPU(s), no collective"),
                        "delivered": "RGBA8 frame in page-locked host memory (RayTracerEngine.render's image)",
-                       "in_flight": Q, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default")},
+                       "in_flight": Q, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default"),
+                       "render_options": options},
             "rays": {"per_step": int(tot[0] / args.steps), "primary_per_step": int(rays_primary) if world == 1 else None,
                      "shadow_traced_per_step": int(tot[3] / args.steps),
                      "shadow_cast_per_step": int(tot[2] / args.steps),
