@@ -31,8 +31,8 @@ time of K steps bracketed by barrier + device sync.  Shadow rays whose walk is s
 (N.L <= 0: the reference discards their result, Object+Extension.swift:123-141) are
 reported apart (`rays.shadow_cast`), never in `value`.
 
-roofline (dominant kernel = the render megakernel, average duration from HIP events on
-its stream, taken inside rt_render): `achieved` = measured HBM bytes per launch (PMC
+roofline (dominant kernel = the render megakernel - for C5 the compacted bounce render's chain of
+launches per frame - average duration from HIP events on its stream, taken inside rt_render): `achieved` = measured HBM bytes per launch (PMC
 FETCH_SIZE x2 + WRITE_SIZE, profiles/roofline_<config>.json, same build) / kernel time,
 against the 8 TB/s HBM peak.  The kernel is not HBM-bound (its working set sits in L2 and
 the 256 MB Infinity Cache): `roofline.binding` names the resource that binds it (FP64 VALU
@@ -460,6 +460,12 @@ def roofline_fields(args, eng, dev, first, step, rows, W, kernel_ms, rays_rank, 
     if prof is not None and world == 1:
         traffic = prof["hbm_bytes_per_launch"]
         r["traffic_source"] = os.path.relpath(ppath, ROOT)
+        r["profiled_kernels"] = prof.get("kernel")
+        if prof.get("frame_chain"):
+            # C5's compacted bounce render: a frame is a chain of launches; traffic and the
+            # compute figures are per frame over the chain (tools/pmc_roofline.py), kernel_ms the
+            # HIP events around the whole chain
+            r["frame_chain"] = prof.get("chain")
         r["profile_build_matches"] = prof.get("lib_sha256_16") == lib_sha
         if r["profile_build_matches"]:
             # figures from another build's profile would describe that build: only a profile of

@@ -200,7 +200,7 @@ int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
  *   unified (1)          one-stack TLAS+BLAS walks; 0 = the nested walk of intersectTLAS
  *   unified_transformed (1)  one-stack walk of instanced scenes (device.h ut_walk)
  *   compact_records (1), compact_tris (1)   float32 records / triangles when exact
- *   xcd_group (0 = auto) tiles per XCD run      queue (0)  compacted bounce render
+ *   xcd_group (0 = auto) tiles per XCD run      queue (1)  compacted bounce render (0 = megakernel)
  *   queue_levels (-1)    timing probe           hitlog (-1 = auto) logged hits per pixel
  *   nodeshade (1), levels (1), tree_ppw (4)     full trace() pass structure
  *   full_flights (4)     full trace() renders overlapping on slot streams

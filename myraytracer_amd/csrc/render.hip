@@ -887,7 +887,7 @@ static const OptDef kOptDefs[kOptCount] = {
     {"compact_records", 1, 0, 1},         // float32-bound BLAS records when exact (layout.h CRec)
     {"compact_tris", 1, 0, 1},            // float32-vertex triangles when exact (layout.h CTri)
     {"xcd_group", 0, 0, 64},              // tiles per XCD run (device.h xcd_tile); 0 = max(2, width / 960)
-    {"queue", 0, 0, 1},                   // compacted bounce render for mirror scenes (k_qscan / k_bounce)
+    {"queue", 1, 0, 1},                   // compacted bounce render for mirror scenes (k_qscan / k_bounce)
     {"queue_levels", -1, -1, 15},         // timing probe: bounce levels of the compacted render (-1 = all)
     {"hitlog", -1, -1, 64},               // closest hits logged per pixel for render_full (-1 = sized automatically)
     {"nodeshade", 1, 0, 1},               // node-parallel shading of logged hits (render_full.h k_shade)

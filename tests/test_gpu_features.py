@@ -311,9 +311,9 @@ def _rough_mirror_scene(w=128, h=96):
 
 @pytest.mark.parametrize("queue", [0, 1])
 def test_queued_bounces_against_the_oracle(queue):
-    """Mirror/conductor scenes through the compacted bounce render (option queue = 1, opt-in:
+    """Mirror/conductor scenes through the compacted bounce render (option queue = 1, the default:
     primary pass + one k_bounce launch per level, rays resolved backward through their queue
-    records) and through the bounce megakernel (0, the default): both equal the oracle's recursion
+    records) and through the bounce megakernel (0): both equal the oracle's recursion
     (Object+Extension.swift:189-206, 252-283).  Covers the general walk (a transformed
     instance), rough mirrors, spp 3 (one traced sample divided by 3), the unified walk with 15
     queue levels, chunk selections, and several replicas."""

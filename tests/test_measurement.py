@@ -59,6 +59,22 @@ def test_overlap_summary_union_and_concurrency():
                                               {"calls": 1, "total_ms": 1.0}}
 
 
+def test_overlap_summary_frame_chain():
+    """C5's frame chain: bounce-level launches inside the timed window join the union."""
+    K = "render_kernel<false, false, 1, false>"
+    spans = [(0, 1_000_000, None),                      # skipped
+             (2_000_000, 6_000_000, None),              # timed frame 1: primary pass
+             (6_000_000, 8_000_000, "k_bounce<1>"),     # its bounce level
+             (9_000_000, 12_000_000, None),             # timed frame 2
+             (12_000_000, 13_000_000, "k_bounce<1>"),
+             (20_000_000, 21_000_000, None),            # a single frame after the timed ones
+             (21_000_000, 22_000_000, "k_bounce<1>")]   # its level: outside the window
+    res = overlap_summary.summarize(_trace_rows(spans, K), K, skip=1, frames=2, extra_kernels=("k_bounce<1>",))
+    # union [2, 8) + [9, 13) = 10 ms over 2 frames
+    assert res["union_per_frame_ms"] == pytest.approx(5.0, rel=1e-6)
+    assert res["other_kernels_in_window"] == {}
+
+
 def test_overlap_summary_needs_enough_dispatches():
     with pytest.raises(SystemExit):
         overlap_summary.summarize(_trace_rows([(0, 1, None)]), "render_kernel", skip=1, frames=1)
@@ -112,3 +128,43 @@ def test_pmc_roofline_summary(tmp_path):
     assert r["lane_throughput_frac"] == pytest.approx(r["valu_busy"] * r["valu_lane_util"], abs=1e-4)
     assert r["valu_insts_per_launch"] == 300_000_000
     assert len(r["lib_sha256_16"]) == 16
+
+
+def test_pmc_roofline_frame_chain(tmp_path):
+    """A frame of several launches (C5's compacted bounce render): per-frame sums over the chain."""
+    K0, K1 = "render_kernel<false, false, 1, true>", "k_bounce<1>"
+    n0, n1 = f"void myrt::dev::{K0}(myrt::RenderParams)", f"void myrt::dev::{K1}(myrt::RenderParams, int)"
+    # 2 frames: one primary pass and 4 bounce levels each
+    _write_csv(str(tmp_path / "trace/x/1_kernel_stats.csv"),
+               [{"Name": n0, "Calls": "2", "TotalDurationNs": "5000000", "AverageNs": "2500000.0"},
+                {"Name": n1, "Calls": "8", "TotalDurationNs": "2000000", "AverageNs": "250000.0"}])
+
+    def pmc(sub, counters):
+        rows, d = [], 0
+        for name, launches, scale in ((n0, 2, 1.0), (n1, 8, 0.1)):
+            for _ in range(launches):
+                d += 1
+                for c, v in counters.items():
+                    rows.append({"Dispatch_Id": str(d), "Kernel_Name": name, "Counter_Name": c,
+                                 "Counter_Value": str(v * scale)})
+        _write_csv(str(tmp_path / sub / "x/1_counter_collection.csv"), rows)
+    pmc("fetch", {"FETCH_SIZE": 100000.0})
+    pmc("write", {"WRITE_SIZE": 10000.0})
+    pmc("td", {"GRBM_GUI_ACTIVE": 10_000_000.0, "TD_TD_BUSY_sum": 200_000_000.0, "TA_BUSY_avr": 500_000.0})
+    pmc("valu", {"GRBM_GUI_ACTIVE": 10_000_000.0, "SQ_ACTIVE_INST_VALU": 200_000_000.0,
+                 "SQ_THREAD_CYCLES_VALU": 6_400_000_000.0, "SQ_INSTS_VALU": 100_000_000.0})
+    lib = tmp_path / "lib.so"
+    lib.write_bytes(b"not a library")
+    out = tmp_path / "roofline.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_roofline.py"), "--kernel", K0, "--kernel", K1,
+                    "--trace", str(tmp_path / "trace"), "--fetch", str(tmp_path / "fetch"),
+                    "--write", str(tmp_path / "write"), "--td", str(tmp_path / "td"), "--valu", str(tmp_path / "valu"),
+                    "--lib", str(lib), "-o", str(out)], check=True, capture_output=True)
+    r = json.loads(out.read_text())
+    per_frame = 1.0 + 4 * 0.1                          # one primary pass + four levels at 0.1 each
+    assert r["frame_chain"] and r["trace_frames"] == 2 and r["pmc_frames"] == 2
+    assert r["kernel_ms"] == pytest.approx(3.5)        # (5 + 2) ms over 2 frames
+    assert r["hbm_bytes_per_launch"] == int(per_frame * (100000 * 1024 * 2 + 10000 * 1024))
+    assert r["valu_busy"] == pytest.approx(200e6 / 256 / (10e6 / 8), abs=1e-4)   # ratios of the chain's sums
+    assert r["valu_lane_util"] == pytest.approx(6.4e9 / (64 * 200e6), abs=1e-4)
+    assert r["chain"][K1]["calls_per_frame"] == 4

@@ -3,15 +3,21 @@
 # profiles of C3/C5 (tools/prof_session.sh), the bench loop's kernel overlap
 # (tools/overlap_session.sh), a one-pass VALU PMC of the full trace() frames (C3g, C3r), smoke,
 # bench lines of every config and the GPU suite.
-# usage: gpurun -- 'bash tools/final_session.sh TAG'  ->  gpurun_out/TAG_*
+# usage: gpurun -- 'bash tools/final_session.sh TAG [1|2]'  ->  gpurun_out/TAG_*
+#   part 1 = the PMC / kernel-trace / overlap profiles, part 2 = smoke, bench lines, full-trace
+#   profiles and the GPU suite (each fits one gpurun call); no part = both
 set -u
 T="${1:-r04z}"
+PART="${2:-all}"
 G="python3 bench.py --steps 10 --warmup 2 --in-flight 1 --no-cpu-baseline --no-side-paths"
 VALU="GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY"
+if [ "$PART" != 2 ]; then
 bash tools/prof_session.sh ${T}_c3 || exit $?
 bash tools/prof_session.sh ${T}_c5 --config c5 || exit $?
 bash tools/overlap_session.sh ${T}_c3 c3 300 || exit $?
 bash tools/overlap_session.sh ${T}_c5 c5 100 || exit $?
+fi
+[ "$PART" = 1 ] && exit 0
 bash tools/gpu_session.sh \
  "${T}_smoke|300|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
  "${T}_bc3|300|python3 bench.py > gpurun_out/${T}_bench_c3.json" \

@@ -6,14 +6,17 @@
 #   -> gpurun_out/TAG_pipe/ (trace), TAG_pipe_bench.json, TAG_bench.json, TAG_overlap.json
 set -u
 tag="$1"; cfg="$2"; steps="$3"; warm="${4:-50}"
+KX=""
 case "$cfg" in
-  c5) K="${KERNEL:-render_kernel<false, true, 1, false>}" ;;
+  # C5 (render option queue = 1): the queued primary pass + the per-level launches of its frame
+  c5) K="${KERNEL:-render_kernel<false, false, 1, true>}"
+      KX="--extra-kernel k_qcount --extra-kernel k_qscan --extra-kernel 'k_bounce<1>' --extra-kernel k_queue_reset" ;;
   *)  K="${KERNEL:-render_kernel<false, false, 1, false>}" ;;
 esac
 B="python3 bench.py --config $cfg --steps $steps --warmup $warm --no-cpu-baseline --no-side-paths"
 s=(
   "${tag}_bench|400|$B > gpurun_out/${tag}_bench.json"
   "${tag}_pipe|400|rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${tag}_pipe -- $B > gpurun_out/${tag}_pipe_bench.json"
-  "${tag}_overlap|120|python3 tools/overlap_summary.py --trace gpurun_out/${tag}_pipe --kernel '$K' --skip $((warm + 16)) --frames $steps --bench gpurun_out/${tag}_pipe_bench.json --lib myraytracer_amd/libmyrt.so -o gpurun_out/${tag}_overlap.json"
+  "${tag}_overlap|120|python3 tools/overlap_summary.py --trace gpurun_out/${tag}_pipe --kernel '$K' $KX --skip $((warm + 16)) --frames $steps --bench gpurun_out/${tag}_pipe_bench.json --lib myraytracer_amd/libmyrt.so -o gpurun_out/${tag}_overlap.json"
 )
 bash "$(dirname "$0")/gpu_session.sh" "${s[@]}"

@@ -16,6 +16,11 @@ are [Q+W, Q+W+K).  Over those:
   time_at_overlap     fraction of the union spent with exactly n launches running
   mean_launch_ms      average launch duration in the pipelined loop (each launch's own
                       interval stretches when it shares the GPU with its neighbours)
+Frame chains (--extra-kernel, repeatable: C5's compacted bounce render, whose frame is the queued
+primary pass plus per-level k_qcount / k_qscan / k_bounce launches): the window runs from the first
+timed primary dispatch's start to the start of the first primary dispatch after the timed ones,
+and every dispatch of the extra kernels starting inside it joins the union (the frames in flight
+at either edge make this approximate to about one frame in `frames`).
 With --bench the same run's bench line is read for ms_per_step (value's clock) and the
 union per frame is compared with it (reference: RayTracer.swift:166,197-203 time the
 whole render).
@@ -47,6 +52,15 @@ def summarize(trace_rows, kernel, skip, frames, extra_kernels=()):
     sel = rk[skip:skip + frames]
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in sel)
     t0, t1 = iv[0][0], max(e for _, e in iv)
+    if extra_kernels:
+        tend = int(rk[skip + frames]["Start_Timestamp"]) if len(rk) > skip + frames else None
+        for r in trace_rows:
+            if any(k in r["Kernel_Name"] for k in extra_kernels) and kernel not in r["Kernel_Name"]:
+                s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                if s_ >= t0 and (tend is None or s_ < tend):
+                    iv.append((s_, e_))
+        iv.sort()
+        t1 = max(e for _, e in iv)
     # sweep: +1 at a start, -1 at an end (ends first at equal times: [start, end) intervals)
     ev = sorted([(s, 1) for s, _ in iv] + [(e, -1) for _, e in iv], key=lambda x: (x[0], x[1]))
     cur, last, union, peak = 0, t0, 0, 0
@@ -60,7 +74,7 @@ def summarize(trace_rows, kernel, skip, frames, extra_kernels=()):
         last = t
     durs = [e - s for s, e in iv]
     res = {
-        "kernel": kernel, "frames": frames, "skipped": skip, "dispatches_seen": len(rk),
+        "kernel": kernel, "extra_kernels": list(extra_kernels), "frames": frames, "skipped": skip, "dispatches_seen": len(rk),
         "span_per_frame_ms": round((t1 - t0) / frames / 1e6, 5),
         "union_per_frame_ms": round(union / frames / 1e6, 5),
         "concurrency": round(sum(durs) / union, 3),
@@ -74,7 +88,7 @@ def summarize(trace_rows, kernel, skip, frames, extra_kernels=()):
     others = {}
     for r in trace_rows:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        if s >= t0 and e <= t1 and kernel not in r["Kernel_Name"]:
+        if s >= t0 and e <= t1 and kernel not in r["Kernel_Name"] and not any(k in r["Kernel_Name"] for k in extra_kernels):
             k = r["Kernel_Name"]
             o = others.setdefault(k, [0, 0])
             o[0] += 1
@@ -87,13 +101,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace", required=True)
     ap.add_argument("--kernel", required=True)
+    ap.add_argument("--extra-kernel", action="append", default=[], help="other kernels of a frame chain")
     ap.add_argument("--skip", type=int, required=True)
     ap.add_argument("--frames", type=int, required=True)
     ap.add_argument("--bench", default=None, help="the same run's bench JSON line (file)")
     ap.add_argument("--lib", default=None, help="the libmyrt.so the trace measured (its sha256 prefix is recorded)")
     ap.add_argument("-o", "--out", required=True)
     a = ap.parse_args()
-    res = summarize(rows(a.trace), a.kernel, a.skip, a.frames)
+    res = summarize(rows(a.trace), a.kernel, a.skip, a.frames, tuple(a.extra_kernel))
     if a.lib:
         import hashlib
         with open(a.lib, "rb") as fh:

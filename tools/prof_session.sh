@@ -5,9 +5,13 @@
 set -u
 tag="$1"; shift
 B="python3 bench.py --steps 20 --warmup 3 --in-flight 1 --no-cpu-baseline --no-side-paths $*"
-# the frame's render kernel: <COUNT, BOUNCE, WALK (1 = identity, 2 = transformed), QUEUE>
+# the frame's render kernel: <COUNT, BOUNCE, WALK (1 = identity, 2 = transformed), QUEUE>; C5 (mirror
+# scene, render option queue = 1) is a frame chain: the queued primary pass, then per level
+# k_qcount / k_qscan / k_bounce, then k_queue_reset (tools/pmc_roofline.py sums it per frame)
+KX=""
 case " $* " in
-  *" --config c5 "*) K="${KERNEL:-render_kernel<false, true, 1, false>}" ;;
+  *" --config c5 "*) K="${KERNEL:-render_kernel<false, false, 1, true>}"
+                     KX="--kernel k_qcount --kernel k_qscan --kernel 'k_bounce<1>' --kernel k_queue_reset" ;;
   *" --config c3i "*) K="${KERNEL:-render_kernel<false, false, 2, false>}" ;;
   *" --config c3g "*|*" --config c3r "*) K="${KERNEL:-render_full<false, false, 1>}" ;;
   *) K="${KERNEL:-render_kernel<false, false, 1, false>}" ;;
@@ -21,6 +25,6 @@ steps=(
   "${tag}_sq|300|timeout -s KILL 240 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS --output-format csv -d gpurun_out/${tag}_sq -- $B"
   "${tag}_mix|300|timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM --output-format csv -d gpurun_out/${tag}_mix -- $B"
   "${tag}_ta|300|timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_ADDR_STALLED_BY_TD_CYCLES_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum --output-format csv -d gpurun_out/${tag}_ta -- $B"
-  "${tag}_roofline|60|python3 tools/pmc_roofline.py --kernel '$K' --trace gpurun_out/${tag}_trace --fetch gpurun_out/${tag}_fetch --write gpurun_out/${tag}_write --td gpurun_out/${tag}_td --valu gpurun_out/${tag}_valu --sq gpurun_out/${tag}_sq --lib myraytracer_amd/libmyrt.so -o gpurun_out/${tag}_roofline.json"
+  "${tag}_roofline|60|python3 tools/pmc_roofline.py --kernel '$K' $KX --trace gpurun_out/${tag}_trace --fetch gpurun_out/${tag}_fetch --write gpurun_out/${tag}_write --td gpurun_out/${tag}_td --valu gpurun_out/${tag}_valu --sq gpurun_out/${tag}_sq --lib myraytracer_amd/libmyrt.so -o gpurun_out/${tag}_roofline.json"
 )
 bash "$(dirname "$0")/gpu_session.sh" "${steps[@]}"
