@@ -195,7 +195,7 @@ __device__ __forceinline__ lds_f64* pix_slot(int k) {
 // QUEUE (primary pass of the compacted bounce render, !BOUNCE): a mirror/conductor hit writes
 // its reflected ray to its pixel's level-1 record (slot `qtile * 64 + lane`, qtile = this wave's
 // tile) and sets `deferred`; k_bounce delivers that pixel.  The PCG32 state is read from
-// pixel slot 3 (the caller parks it there) and (i, j) give its stream.
+// pixel slot 3 (the caller parks it there) and (i0, j0) + the lane give its stream.
 // The bounce megakernel (C5's mirror scenes) walks the four-wide tree too, at 4 waves/SIMD
 // (MYRT_BOUNCE_WPE): C5 5020 vs 4733 Mrays/s for the binary walk at 6 waves, which was the binary
 // walk's best occupancy; the wide walk at 5 waves spills (4142), DESIGN.md §4.
@@ -204,7 +204,7 @@ __device__ __forceinline__ lds_f64* pix_slot(int k) {
 #endif
 template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
-                         Counts& c, bool park_rng, int i = 0, int j = 0,
+                         Counts& c, bool park_rng, int i0 = 0, int j0 = 0,
                          bool* deferred = nullptr, int qtile = 0) {
     static_assert(!(QUEUE && BOUNCE), "the queued primary pass has no bounce loop");
     auto park = [&]() { if (BOUNCE && park_rng) *pix_slot(3) = __builtin_bit_cast(double, rng.state); };
@@ -236,14 +236,17 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         const V3 N = frontFacing ? Ngeo : -Ngeo;
         const bool computeDirect = !(M.ior > 0) || frontFacing;
         V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
-        long long q = -1;
-        if (QUEUE) {     // the bounce ray is formed before the shadow walks: only q stays live
+        bool queued = false;
+        if (QUEUE) {     // the bounce ray is formed before the shadow walks: only a flag stays live
             const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && P.max_depth > 0;
             const unsigned long long m = __ballot(want);
             if (m) {
                 if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) P.bmask[qtile] = m;
                 if (want) {
-                    q = (long long)qtile * 64 + (threadIdx.x & 63);
+                    const int l = pix_lane();                     // the lane's pixel, recomputed
+                    const int i = i0 + l % kTileW, j = j0 + l / kTileW;
+                    const long long q = (long long)qtile * 64 + l;
+                    queued = true;
                     PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*pix_slot(3)),
                                             pixel_seed(i, j));
                     queue_write(P, q, M, d, N, p, r, time, i, j);
@@ -253,8 +256,8 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         }
         if (computeDirect)
             point_lights<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE>(P, M, N, p, d, time, st, c, Lo, park, unpark);
-        if (QUEUE && q >= 0) {
-            queue_write_lo(P, q, Lo);
+        if (QUEUE && queued) {
+            queue_write_lo(P, (long long)qtile * 64 + pix_lane(), Lo);
             *deferred = true;
             L = v3(0, 0, 0);
             break;
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             // across the walks; the memory clobber makes the reloads real loads.
             if (!BOUNCE) *pix_slot(3) = __builtin_bit_cast(double, rng.state);
             const V3 col = trace_path<COUNT, BOUNCE, WALK, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt, true,
-                                                                 ii, jj, &deferred, tile);
+                                                                 i0, j0, &deferred, tile);
             asm volatile("" ::: "memory");
             if (!BOUNCE) {
                 const int l2 = pix_lane();
@@ -1069,6 +1072,9 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
                               hipHostMallocMapped));
         HIP_TRY(hipHostGetDevicePointer((void**)&f.host_counters_dev, f.host_counters, 0));
     }
+    // the zeroing above ran on the null stream, which does not order against the non-blocking
+    // render streams: finish it before any render can start
+    HIP_TRY(hipDeviceSynchronize());
     return RT_OK;
 }
 
@@ -1460,7 +1466,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
 // pixels trace one sample (Int(sqrt(spp)) == 1) with maxRecursionDepth <= kMaxQueueLevels;
 // `arena` grows to levels x (tiles x 64) records, the tile masks and k_qscan's tile list
 // (false: allocation refused or failed -> the bounce megakernel).
-static bool queue_arena(const rt_scene* s, BounceArena* arena, RenderParams& P, int64_t tiles) {
+static bool queue_arena(const rt_scene* s, BounceArena* arena, RenderParams& P, int64_t tiles, hipStream_t stream) {
     if (!arena || s->opt[kOptQueue] == 0) return false;
     if (P.cam.n != 1 || P.max_depth < 1 || P.max_depth > kMaxQueueLevels) return false;
     const int64_t levels = P.max_depth;
@@ -1477,7 +1483,11 @@ static bool queue_arena(const rt_scene* s, BounceArena* arena, RenderParams& P, 
         (void)hipFree(arena->base);
         arena->base = nullptr;
         arena->levels = arena->tiles = 0;
-        if (hipMalloc(&arena->base, bytes(lv, tl)) != hipSuccess || hipMemset(arena->base, 0, bytes(lv, tl)) != hipSuccess) {
+        // zeroed on the render's own stream: a plain hipMemset runs on the null stream, which does
+        // not order against the library's non-blocking streams - it could zero the masks and
+        // records while this render's kernels already use them (undelivered mirror pixels)
+        if (hipMalloc(&arena->base, bytes(lv, tl)) != hipSuccess ||
+            hipMemsetAsync(arena->base, 0, bytes(lv, tl), stream) != hipSuccess) {
             (void)hipGetLastError();
             (void)hipFree(arena->base);
             arena->base = nullptr;
@@ -1524,7 +1534,7 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
         else M_(dev::kWalkGeneral);                                         \
     } while (0)
-    if (bounce && !count && queue_arena(s, arena, P, (int64_t)grid.x * (bt / 64))) {
+    if (bounce && !count && queue_arena(s, arena, P, (int64_t)grid.x * (bt / 64), stream)) {
         // primary + shadow rays of every pixel in the spill-free primary instantiation, then per
         // level the tile list (k_qscan) and the level's rays in coherent batches (k_bounce)
 #define MYRT_QPRIM(W_) hipLaunchKernelGGL((dev::render_kernel<false, false, W_, true>), grid, block, lds, stream, P)
