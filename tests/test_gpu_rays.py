@@ -255,6 +255,73 @@ def test_equal_t_ties_between_instances(walk):
         assert st.rewalked == 0
 
 
+def _transformed_instances():
+    """Instances of one mesh under scales, rotations and translations - triangles only, nothing
+    moving."""
+    sc = scenes.scaled(scenes.scene_c2(inline=True), 8, 8)
+    base = sc.objects[0]
+    rng = np.random.RandomState(31)
+    objs = [base]
+    for k in range(5):
+        Rm = _rotation(rng) * (0.4 + 0.5 * k)
+        t = rng.uniform(-3.0, 3.0, size=3)
+        M4 = np.eye(4)
+        M4[:3, :3] = Rm
+        M4[:3, 3] = t
+        objs.append(M.MeshInstance(id=40 + k, base_mesh_id=base.id, material="1",
+                                   transform=tuple(M4.T.reshape(-1))))
+    sc.objects = objs
+    return sc
+
+
+@pytest.mark.parametrize("walk", ["transformed", "nested"])
+def test_transformed_mesh_instances(walk):
+    """Rotated / scaled / translated mesh instances: the unified transformed walk (device.h
+    ut_walk) and the nested walk give the oracle's intersectTLAS / occludedTLAS bit for bit -
+    including axis-aligned and signed-zero directions in local space."""
+    sc = _transformed_instances()
+    O, D = _ray_set(np.array([0.0, 0.0, 0.0]), 4.0, 3000, 23)
+    _check_closest(sc, O, D, walk=walk)
+    _check_occluded(sc, O, D, np.random.RandomState(6).uniform(0.1, 8.0, size=len(O)), walk=walk)
+
+
+@pytest.mark.parametrize("walk", ["transformed", "nested"])
+def test_equal_t_ties_between_transformed_instances(walk):
+    """Two instances of one mesh under the same rotation and scale, with different materials:
+    every hit is a tie between them, and the walks must return the reference's instance (the
+    first intersectTLAS visits; strict t < hit.t, RTContext.swift:494)."""
+    hp, hf = scenes.heightfield(24, 8.0, 1.0, 3)
+    hp32 = hp.astype(np.float32).astype(np.float64)
+    a = M.Mesh(id=1, material="1", positions=hp32, indices=hf.astype(np.int32), indices_one_based=False,
+               shading_mode="flat")
+    c, sn = np.cos(0.5), np.sin(0.5)                    # about y, so the camera still sees the grid
+    Mt = np.eye(4)
+    Mt[:3, :3] = np.array([[c, 0.0, sn], [0.0, 1.0, 0.0], [-sn, 0.0, c]]) * 0.75
+    Mt[:3, 3] = (0.25, -0.5, 0.125)
+    T = tuple(Mt.T.reshape(-1))
+    sc = scenes.scaled(scenes.scene_c1(8, 8), 48, 40)
+    sc.materials = [sc.materials[0], dataclasses.replace(sc.materials[0], diffuse=(0.1, 0.9, 0.2))]
+    sc.objects = [a, M.MeshInstance(id=5, base_mesh_id=1, material="1", transform=T),
+                  M.MeshInstance(id=6, base_mesh_id=1, material="2", transform=T)]
+    sc.cameras[0].position = (0.5, 7.0, 7.5)
+    sc.cameras[0].gaze_point = (0.0, 0.0, 0.0)
+    sc.point_lights[0].position = (1.0, 9.0, 2.0)
+    rng = np.random.RandomState(4)
+    D = rng.normal(size=(3000, 3)) * np.array([0.4, 1.0, 0.4]) - np.array([0.0, 2.0, 0.0])
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    loc = hp32[rng.randint(len(hp32), size=3000)] + rng.uniform(-0.05, 0.05, size=(3000, 3)) * np.array([1, 0, 1])
+    tgt = loc @ Mt[:3, :3].T + Mt[:3, 3]
+    O = tgt - 12.0 * D
+    hit = _check_closest(sc, O, D, walk=walk)
+    assert hit.mean() > 0.3
+    eng = _engine(sc, walk)
+    rgb, rgba, st = eng.render_rows(0, 0, 1, True)
+    ref, ref8, _ = oracle.OracleScene(sc).render(0, 0, 1, threads=0, rgba=True)
+    eng.close()
+    assert float(np.abs(rgb - ref).max()) <= 1e-5 and np.array_equal(rgba, ref8)
+    assert st.rewalked == 0                          # the transformed walks keep the reference order
+
+
 def test_fast_reciprocal_is_ieee_division():
     """device.h rcp_rn (1/det of the triangle tests when RenderParams::fast_rcp holds) equals
     IEEE 1.0/x bit for bit over its range 2^-700 <= |x| <= 2^1000: random mantissas at every
