@@ -787,8 +787,8 @@ struct BounceArena {
 };
 // Compacted bounce render: device bytes one launch may take for its queues (else the megakernel)
 constexpr int64_t kQueueBytesCap = 16ll << 30;
-// (The compacted bounce render is off by default, option queue: parity-green but slower than the
-// bounce megakernel on C5, DESIGN.md §4 "Compacted bounce render".)
+// (The compacted bounce render is the default since round 4, option queue: faster pipelined than
+// the bounce megakernel on C5, slower one frame alone, DESIGN.md §4 "Compacted bounce render".)
 // Scratch of the full trace() passes (render_full.h), grown on demand: per-pixel area-light
 // event counts and jitter prefixes, the closest-hit log, the node-parallel shading records and
 // the level passes' node flags.  The replica has one (rt_render, in-order renders) and each

@@ -28,13 +28,14 @@ def run(out, k=8):
     return ms
 
 
-for zc in ("0", "1"):
-    for nb in ("1", "2", "4", "8"):
-        os.environ["MYRT_ZEROCOPY"], os.environ["MYRT_BATCHES"] = zc, nb
+for zc in (0, 1):                                   # render options zerocopy / batches
+    for nb in (1, 2, 4, 8):
+        eng.set_option("zerocopy", zc)
+        eng.set_option("batches", nb)
         ms = run(pin)
         print(f"pinned zerocopy={zc} batches={nb}: {ms:.3f} ms  {rays / ms / 1e3:.0f} Mrays/s", flush=True)
-os.environ["MYRT_ZEROCOPY"] = "0"
-for nb in ("2", "4", "8"):
-    os.environ["MYRT_BATCHES"] = nb
+eng.set_option("zerocopy", 0)
+for nb in (2, 4, 8):
+    eng.set_option("batches", nb)
     ms = run(pag)
     print(f"pageable batches={nb}: {ms:.3f} ms  {rays / ms / 1e3:.0f} Mrays/s", flush=True)

@@ -1,5 +1,6 @@
-"""Kernel time of the C3 (or C5) frame under runtime switch combinations (A/B in one process).
-usage: probe_env.py c3 "MYRT_BLOCK=64 MYRT_XCD=4" "MYRT_BLOCK=64 MYRT_ORDER=1" ..."""
+"""Kernel time of the C3 (or C5 ...) frame under render-option combinations (rt_scene_set_option,
+INTEGRATION.md table), A/B in one process; each combination starts from the defaults.
+usage: probe_options.py c3 "xcd_group=4" "wide=0 compact_records=0" ..."""
 import os
 import sys
 
@@ -17,8 +18,7 @@ eng = M.RayTracerEngine(sc)
 W, H = sc.cameras[0].image_resolution
 stream = torch.cuda.current_stream()
 out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
-KEYS = ("MYRT_BLOCK", "MYRT_XCD", "MYRT_ROTATE", "MYRT_COMPACT", "MYRT_CTRI", "MYRT_QUEUE", "MYRT_UT", "MYRT_UNIFIED", "MYRT_HITLOG",
-        "MYRT_NODESHADE")
+DEFAULTS = {}
 
 
 def t_frame(k=20):
@@ -36,11 +36,12 @@ def t_frame(k=20):
 
 for rep in range(2):
     for combo in sys.argv[2:]:
-        for key in KEYS:
-            os.environ.pop(key, None)
+        for k, v in DEFAULTS.items():
+            eng.set_option(k, v)
         for kv in combo.split():
             k, v = kv.split("=")
-            os.environ[k] = v
+            DEFAULTS.setdefault(k, eng.get_option(k))
+            eng.set_option(k, int(v))
         ms = t_frame()
         import hashlib
         sha = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]

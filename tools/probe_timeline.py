@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 FIRST = int(sys.argv[2]) if len(sys.argv) > 2 else 0     # chunk selection (a rank's C4 share)
 STEP = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-TAG = os.environ.get("MYRT_ORDER", "0")
+TAG = sys.argv[4] if len(sys.argv) > 4 else "0"       # label of the run
 sc = scenes.scene_c3(path_dir=os.path.join(ROOT, "scenes_cache")) if cfg == "c3" else \
     scenes.scene_c5(path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
@@ -50,7 +50,7 @@ print("resident waves every 5% of the span:", " ".join(str(int(a)) for a in act[
 # waves that start in the last 25% of the span and their durations
 late = st > 0.75 * span
 print(f"waves starting in the last 25%: {late.sum()}, mean duration {dur[late].mean() if late.any() else 0:.4f} ms", flush=True)
-wpb = int(os.environ.get("MYRT_BLOCK", "64")) // 64
+wpb = 1                                                 # one-wave blocks (render.hip kRenderBlock)
 gx = (W + 8 * wpb - 1) // (8 * wpb)
 top = np.argsort(-dur)[:10]
 for k in top:
