@@ -479,24 +479,7 @@ struct WideBuilder {
     std::vector<std::vector<WItem>> groups;
     int depth = 0, max_depth = 0;        // wide levels on the current path / deepest
     explicit WideBuilder(HostScene& s) : S(s) {}
-#ifndef MYRT_WIDE_MERGE
-#define MYRT_WIDE_MERGE 0
-#endif
-    // (variant) a BLAS record whose two children are adjacent leaf runs becomes ONE slot with the
-    // record's box; the walk tests both runs (each candidate still needs its own run's exact box)
-    bool is_pair(const WItem& x) const {
-        if (!MYRT_WIDE_MERGE || x.group >= 0 || x.ref < 0 || (int64_t)x.ref >= S.blas_records) return false;
-        const WRec& r = S.recs[x.ref];
-        if (r.ref[0] >= 0 || r.ref[1] >= 0) return false;
-        const int64_t a = ~(int64_t)r.ref[0], b = ~(int64_t)r.ref[1];
-        if (a >= S.tlas_leaf_base || b >= S.tlas_leaf_base || b >= (int64_t(1) << 30)) return false;
-        int64_t e = a;
-        while (!S.tris[e].last) ++e;
-        return b == e + 1;
-    }
-    bool terminal(const WItem& x) const {
-        return (x.group < 0 && x.ref < 0 && (int64_t)~x.ref < S.tlas_leaf_base) || is_pair(x);
-    }
+    bool terminal(const WItem& x) const { return x.group < 0 && x.ref < 0 && (int64_t)~x.ref < S.tlas_leaf_base; }
     static double area(const WItem& x) {
         const double dx = x.hi[0] - x.lo[0], dy = x.hi[1] - x.lo[1], dz = x.hi[2] - x.lo[2];
         return dx * dy + dy * dz + dz * dx;
@@ -580,26 +563,12 @@ struct WideBuilder {
             c.erase(c.begin() + best);
             c.insert(c.begin() + best, e.begin(), e.end());
         }
-#ifndef MYRT_WIDE_SLOT_AREA
-#define MYRT_WIDE_SLOT_AREA 0
-#endif
-        // (variant) slots by descending surface area: the any-hit walks take the first hit slot
-        if (MYRT_WIDE_SLOT_AREA)
-            std::stable_sort(c.begin(), c.end(), [](const WItem& x, const WItem& y) { return area(x) > area(y); });
         const int32_t idx = (int32_t)S.wnodes.size();
         S.wnodes.emplace_back();
         max_depth = std::max(max_depth, ++depth);
         int32_t refs[4] = {0, 0, 0, 0};
         for (size_t i = 0; i < c.size(); ++i) {
-            if (is_pair(c[i])) {
-                const WRec& r = S.recs[c[i].ref];
-                refs[i] = ~(int32_t)(~r.ref[0] | (1 << 30));          // bit 30 of ~ref: a pair
-                for (int q = 0; q < 2; ++q) {
-                    double* b = &S.lbox[6 * (size_t)~r.ref[q]];
-                    for (int k = 0; k < 3; ++k) { b[k] = r.lo[q][k]; b[3 + k] = r.hi[q][k]; }
-                }
-                S.wide_leaves += 2;
-            } else if (terminal(c[i])) {
+            if (terminal(c[i])) {
                 refs[i] = c[i].ref;
                 double* b = &S.lbox[6 * (size_t)~c[i].ref];
                 for (int k = 0; k < 3; ++k) { b[k] = c[i].lo[k]; b[3 + k] = c[i].hi[k]; }

@@ -290,16 +290,10 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
         if (ref >= 0) {
             if (wide_inner<SHADOW>(P, wbase, ref, R, lim, st)) continue;
         } else {
-#ifndef MYRT_WIDE_MERGE
-#define MYRT_WIDE_MERGE 0
-#endif
-            // (variant MYRT_WIDE_MERGE) bit 30 of ~ref: the slot holds this run and the next one
-            bool pair = MYRT_WIDE_MERGE && ((~ref) & (1 << 30));
-            const int tb = MYRT_WIDE_MERGE ? ((~ref) & ~(1 << 30)) : ~ref;
-            int t0 = tb;                                   // the current run's first TriRec (its lbox)
+            const int t0 = ~ref;
             int box = 0;                                   // leaf box: 0 unchecked, 1 passes, 2 fails
             auto run = [&](const auto* tris) {
-                for (int t = tb;; ++t) {
+                for (int t = t0;; ++t) {
                     const auto T = tris[t];                // by value: `last` arrives with the vertices
                     if (COUNT) c.tris++;
                     if (SHADOW) {
@@ -338,10 +332,7 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
                             }
                         }
                     }
-                    if (T.last) {
-                        if (MYRT_WIDE_MERGE && pair) { pair = false; t0 = t + 1; box = 0; continue; }
-                        break;
-                    }
+                    if (T.last) break;
                 }
                 return false;
             };
