@@ -173,7 +173,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo", init_method="env://")   # barriers + scalar reductions only
+        # barriers + scalar reductions only; gloo announces its connections on stdout, which is
+        # kept for the one JSON line: send that chatter to stderr while the group forms
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", init_method="env://")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     # MYRT_BENCH_DEVICE pins every rank to one device: rehearsing N ranks on a 1-GPU box
     dev_override = os.environ.get("MYRT_BENCH_DEVICE")
     local = int(dev_override) if dev_override is not None else local
