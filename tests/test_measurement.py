@@ -168,3 +168,46 @@ def test_pmc_roofline_frame_chain(tmp_path):
     assert r["valu_busy"] == pytest.approx(200e6 / 256 / (10e6 / 8), abs=1e-4)   # ratios of the chain's sums
     assert r["valu_lane_util"] == pytest.approx(6.4e9 / (64 * 200e6), abs=1e-4)
     assert r["chain"][K1]["calls_per_frame"] == 4
+
+
+def test_pmc_valu_kernels_per_kernel_figures(tmp_path):
+    """tools/pmc_valu_kernels.py: per-kernel VALU busy / lane utilisation from one pass."""
+    rows = []
+    for d, (name, act, thr, gui) in enumerate([("void myrt::dev::k_shade<1>(myrt::RenderParams)", 2.56e8, 6.4e9, 8e6),
+                                               ("void myrt::dev::k_level<1>(myrt::RenderParams, int)", 1.28e8, 4.096e9, 8e6)]):
+        for c, v in (("SQ_ACTIVE_INST_VALU", act), ("SQ_THREAD_CYCLES_VALU", thr), ("GRBM_GUI_ACTIVE", gui),
+                     ("SQ_INSTS_VALU", act)):
+            rows.append({"Dispatch_Id": str(d + 1), "Kernel_Name": name, "Counter_Name": c, "Counter_Value": str(v)})
+    _write_csv(str(tmp_path / "valu/x/1_counter_collection.csv"), rows)
+    out = tmp_path / "v.txt"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_valu_kernels.py"), str(tmp_path / "valu"),
+                    "-o", str(out)], check=True, capture_output=True)
+    lines = {l.split()[0]: l.split() for l in out.read_text().splitlines()[1:]}
+    busy = 2.56e8 / 256 / (8e6 / 8)
+    assert float(lines["k_shade<1>"][2]) == pytest.approx(busy, abs=1e-3)
+    assert float(lines["k_shade<1>"][3]) == pytest.approx(6.4e9 / (64 * 2.56e8), abs=1e-3)
+    assert float(lines["k_level<1>"][3]) == pytest.approx(4.096e9 / (64 * 1.28e8), abs=1e-3)
+
+
+def test_isa_loops_census():
+    """tools/isa_loops.py groups instructions by innermost loop header (LLVM loop comments)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_loops
+    asm = """_Zkern:
+\ts_mov_b32 s0, 0
+.LBB0_1:                                ; =>This Loop Header: Depth=1
+\tv_add_f32 v0, v0, v1
+\tv_readlane_b32 s4, v127, 3
+.LBB0_2:                                ;   Parent Loop BB0_1 Depth=1
+                                        ; =>  This Inner Loop Header: Depth=2
+\tscratch_load_dword v2, off, off offset:8 ; 4-byte Folded Reload
+\tv_mul_f32 v2, v2, v2
+; %bb.3:                                ;   in Loop: Header=BB0_1 Depth=1
+\ts_load_dword s1, s[0:1], 0x0
+\tv_writelane_b32 v127, s1, 4
+.Lfunc_end0:
+""".split("\n")
+    rows = isa_loops.census(asm, 1)
+    assert rows["BB0_1"]["depth"] == 1 and rows["BB0_1"]["readlane"] == 1 and rows["BB0_1"]["writelane"] == 1
+    assert rows["BB0_1"]["s_load"] == 1 and rows["BB0_1"]["valu"] == 3
+    assert rows["BB0_2"]["depth"] == 2 and rows["BB0_2"]["scratch_ld"] == 1 and rows["BB0_2"]["valu"] == 1

@@ -20,18 +20,22 @@ import sys
 def census(lines, min_depth=1):
     rows = {}
     depth, hdr = 0, None
-    for l in lines:
-        m = re.match(r'^(\.LBB\S+):', l)
+    n = len(lines)
+    for i, l in enumerate(lines):
+        m = re.match(r'^\.?L?(BB\S+):', l)
         if m or l.startswith('; %bb'):
-            d = re.search(r'Depth=(\d+)', l)
-            depth = int(d.group(1)) if d else 0
-            h = re.search(r'Header=(\S+)', l)
-            if 'Loop Header' in l:
-                hdr = m.group(1).lstrip('.') if m else hdr
-            elif h:
-                hdr = h.group(1)
+            # the label's comment may continue on the following comment-only lines
+            text = l
+            k = i + 1
+            while k < n and re.match(r'^\s+;', lines[k]):
+                text += ' ' + lines[k]
+                k += 1
+            if 'Loop Header' in text and m:
+                hdr = m.group(1)
+                depth = int(re.search(r'Loop Header: Depth=(\d+)', text).group(1))
             else:
-                hdr = None
+                h = re.search(r'Header=(\S+) Depth=(\d+)', text)
+                hdr, depth = (h.group(1), int(h.group(2))) if h else (None, 0)
             continue
         s = l.strip()
         if not s or s.startswith(';') or s.startswith('.') or s.endswith(':'):
@@ -44,8 +48,8 @@ def census(lines, min_depth=1):
         r['insts'] += 1
         if op.startswith('v_'):
             r['valu'] += 1
-        if op.startswith('v_readlane') or op.startswith('v_readfirstlane'):
-            r['readlane'] += op.startswith('v_readlane')
+        if op.startswith('v_readlane'):
+            r['readlane'] += 1
         if op.startswith('v_writelane'):
             r['writelane'] += 1
         if op.startswith('s_load') or op.startswith('s_buffer_load'):
