@@ -208,6 +208,8 @@ int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
  *   batches (0 = auto), zerocopy (1)            rt_render delivery
  *   submit_events (1), submit_counters (1), submit_dma (0)   rt_render_submit delivery
  *   debug_fail_replica (-1)   test hook: inject a launch failure on that replica
+ *   wide_delta_scale (1000)   test hook: the four-wide walk's widening in 1/1000 of the proven
+ *                             bound (wide.h); below 1000 exactness is no longer guaranteed
  * Unknown names and out-of-range values return RT_ERR_INVALID_ARG.  Set options between
  * renders (not while renders of the scene are in flight). */
 int32_t rt_scene_set_option(rt_scene* scene, const char* name, int64_t value);

@@ -880,7 +880,7 @@ enum OptId {
     kOptWide, kOptUnified, kOptUnifiedTransformed, kOptCompactRecords, kOptCompactTris, kOptXcdGroup,
     kOptQueue, kOptQueueLevels, kOptHitlog, kOptNodeshade, kOptLevels, kOptTreePpw, kOptFullFlights,
     kOptDeepCapMb, kOptBatches, kOptZerocopy, kOptSubmitEvents, kOptSubmitCounters, kOptSubmitDma,
-    kOptDebugFailReplica, kOptCount
+    kOptDebugFailReplica, kOptWideDeltaScale, kOptCount
 };
 struct OptDef { const char* name; int64_t def, lo, hi; };
 static const OptDef kOptDefs[kOptCount] = {
@@ -904,6 +904,9 @@ static const OptDef kOptDefs[kOptCount] = {
     {"submit_counters", 1, 0, 1},         // ray counters delivered per submitted render
     {"submit_dma", 0, 0, 2},              // submitted delivery: 0 kernel stores, 1 staging + DMA, 2 staging only
     {"debug_fail_replica", -1, -1, 1 << 20},   // test hook: launch failure injected on this replica
+    {"wide_delta_scale", 1000, 0, 1000000},    // test hook: the four-wide walk's widening (wdelta) in
+                                               // 1/1000 of the exact bound; < 1000 voids wide.h's
+                                               // exactness proof (tests show that it has teeth)
 };
 
 struct rt_scene {
@@ -1181,16 +1184,18 @@ static double dist_to_center(const HostScene& S, const double p[3]) {
 
 // The conservative four-wide walk (wide.h) for this render: every ray origin has coordinates of
 // magnitude <= origin_coord (camera + lens) or lies inside the scene bounds (hit points, offset by
-// shadowRayEpsilon).  wdelta = 8 * 2^-24 * max(|box coordinate|, |origin coordinate|) bounds the
+// shadowRayEpsilon; triangle hit points only: scene.cpp build_wide builds no tree for scenes with
+// spheres or planes, whose hit points can lie outside every box).  wdelta = 8 * 2^-24 * max(|box coordinate|, |origin coordinate|) bounds the
 // FP32 rounding of the slab terms (wide.h header); weps = eps rounded down to float.
-static void set_wide(const HostScene& S, const DeviceReplica& r, RenderParams& P, double origin_coord, bool on) {
+static void set_wide(const HostScene& S, const DeviceReplica& r, RenderParams& P, double origin_coord, bool on,
+                     int64_t scale_permille) {
     P.wnodes = r.wnodes; P.lbox = r.lbox; P.wide_root = S.wide_root;
     const double R = std::max(S.wide_coord, origin_coord) + std::fabs(S.shadow_eps) + std::fabs(S.eps);
-    P.wdelta = R * 0x1p-21;
+    P.wdelta = R * 0x1p-21 * ((double)scale_permille * 1e-3);
     float we = (float)S.eps;
     if ((double)we > S.eps) we = std::nextafter(we, -HUGE_VALF);
     P.weps = we;
-    P.wide = (S.wide_root >= 0 && r.wnodes && R < 0x1p27 && R > 0x1p-60 && std::isfinite(R) &&
+    P.wide = (S.wide_root >= 0 && r.wnodes && !S.has_special && R < 0x1p27 && R > 0x1p-60 && std::isfinite(R) &&
               on) ? 1 : 0;
 }
 
@@ -1251,7 +1256,7 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         const rt_camera& cam0 = S.cams[cam];
         const double ce[3] = {cam0.position.x, cam0.position.y, cam0.position.z};
         set_wide(S, r, P, std::max({std::fabs(ce[0]), std::fabs(ce[1]), std::fabs(ce[2])}) + std::fabs(cam0.aperture_size),
-                 s->opt[kOptWide] != 0);
+                 s->opt[kOptWide] != 0, s->opt[kOptWideDeltaScale]);
     }
     return P;
 }
@@ -2405,7 +2410,7 @@ static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o,
         P.fast_rcp = fast_rcp_for(s->host, 2.0 * dm + 1.0);
         double oc = 0.0;                      // the wide walk's widening for these origins
         for (int32_t k = 0; k < 3 * n; ++k) oc = std::isfinite(o[k]) ? std::max(oc, std::fabs(o[k])) : HUGE_VAL;
-        set_wide(s->host, r, P, oc, s->opt[kOptWide] != 0);
+        set_wide(s->host, r, P, oc, s->opt[kOptWide] != 0, s->opt[kOptWideDeltaScale]);
     }
     dev::RayBatch B{};
     B.n = n;

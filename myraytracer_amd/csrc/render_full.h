@@ -412,20 +412,29 @@ __device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int
 #else
 #define MYRT_FULL_ATTR
 #endif
+// The closest-hit walks' equal-t re-walks (wide.h ties; rt_stats.rewalked) of one wave, counted
+// where the walks run (every lane of the wave must reach this: wave_sum reads all 64 lanes).
+__device__ __forceinline__ void flush_ties(const RenderParams& P, const Counts& c) {
+    const unsigned long long t = wave_sum(c.ties);
+    if ((threadIdx.x & 63) == 0 && t) atomicAdd(&P.counters[kCounterTies], t);
+}
+
 template <bool DEEP, int WALK>
 __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_events(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
-    if (i >= P.cam.width || j >= P.cam.height) return;
     Counts cnt{};
-    MYRT_STACK(st, lds_stack);
-    long long events = 0;
-    const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
-    HitLog hl{P.hits + q, (size_t)P.hit_stride, 0, P.hits ? P.hit_slots : 0};
-    (void)pixel_full<false, true, DEEP, WALK>(P, i, j, events, st, cnt, hl);
-    P.events[q] = events;
-    if (P.walks) P.walks[q] = hl.k;
+    if (i < P.cam.width && j < P.cam.height) {
+        MYRT_STACK(st, lds_stack);
+        long long events = 0;
+        const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
+        HitLog hl{P.hits + q, (size_t)P.hit_stride, 0, P.hits ? P.hit_slots : 0};
+        (void)pixel_full<false, true, DEEP, WALK>(P, i, j, events, st, cnt, hl);
+        P.events[q] = events;
+        if (P.walks) P.walks[q] = hl.k;
+    }
+    flush_ties(P, cnt);
 }
 
 // ---- breadth-first events passes (P.hit_tree != 0) -------------------------------------------
@@ -497,13 +506,22 @@ __device__ __forceinline__ void level_node(const RenderParams& P, size_t q, int 
 }
 
 template <int WALK>
+__device__ __forceinline__ void level_pixel(const RenderParams& P, int level, int i, int j, int slot, int row,
+                                            Counts& cnt);
+template <int WALK>
 __global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_level(RenderParams P, int level) {
-    extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
-    if (i >= P.cam.width || j >= P.cam.height) return;
-    const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
     Counts cnt{};
+    if (i < P.cam.width && j < P.cam.height) level_pixel<WALK>(P, level, i, j, slot, row, cnt);
+    flush_ties(P, cnt);
+}
+
+template <int WALK>
+__device__ __forceinline__ void level_pixel(const RenderParams& P, int level, int i, int j, int slot, int row,
+                                            Counts& cnt) {
+    extern __shared__ unsigned long long lds_stack[];
+    const size_t q = ((size_t)slot * 8 + row) * (size_t)P.cam.width + i;
     if (level > 0) {
         // one wave per tile and traced sample runs the level's node positions one after another
         // (a position's lanes are the same node of neighbouring pixels); a position no lane of
@@ -734,6 +752,7 @@ __global__ __launch_bounds__(256) MYRT_FULL_ATTR void render_full(RenderParams P
         if (s1) atomicAdd(&P.counters[1], s1);
         if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
     }
+    flush_ties(P, cnt);
     if (COUNT) {
         const unsigned long long a = wave_sum(cnt.recs), b = wave_sum(cnt.tris), cc = wave_sum(cnt.normals),
                                  dd = wave_sum(cnt.insts), ee = wave_sum(valid ? 1ull : 0ull);

@@ -600,9 +600,16 @@ struct WideBuilder {
 
 static void build_wide(HostScene& S) {
     S.wnodes.clear();
-    S.lbox.assign(6 * S.tris.size(), 0.0);
+    S.lbox.clear();
+    S.wide_root = -1;
     S.wide_leaves = 0;
     S.wide_coord = 0.0;
+    // The widening bound (render.hip set_wide, wide.h header) needs every ray origin of a render
+    // to lie within wide_coord (the boxes' largest coordinate) or the camera's reach: hit points
+    // on triangles do, hit points on an unbounded plane or a sphere outside the triangle boxes
+    // would not.  So the four-wide tree exists only for triangle-only scenes.
+    if (S.has_special) return;
+    S.lbox.assign(6 * S.tris.size(), 0.0);
     WideBuilder B(S);
     WItem root{};
     for (int k = 0; k < 3; ++k) { root.lo[k] = S.tlas_root_lo[k]; root.hi[k] = S.tlas_root_hi[k]; }
