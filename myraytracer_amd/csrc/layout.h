@@ -70,16 +70,19 @@ static_assert(sizeof(CTri) == 48, "CTri is 48 B");
 // further per render (RenderParams::wdelta) so a conservative FP32 test passes whenever the
 // reference's FP64 test of any leaf below passes.  Leaf boxes are then checked exactly (FP64,
 // lbox) before a hit is accepted.  Slots [axis][child], SoA per axis.
-// Row a of hi lies 64 B after row a of lo, so a lane reads its near and far rows at byte offsets
-// n and n ^ 64 (wide.h WRay).
+// The node array holds EIGHT copies of the tree, one per ray-direction octant o (bit a of o set:
+// d[a] < 0; copy o starts at node o * RenderParams::wide_copy): in copy o a node's rows are
+// already the near and far planes of that octant (near = the box minimum along a when d[a] >= 0,
+// the maximum otherwise) and its slots are in front-to-back order for directions of that octant
+// (scene.cpp wide_octant_copies), so a lane reads fixed rows and visits slots in memory order.
 struct alignas(128) W4Node {
-    float lo[3][4];       // child c box min along axis a: lo[a][c] (rounded down)
-    int32_t ref[4];       // >= 0: W4Node index; < 0: ~first TriRec of a reference leaf run
-    float hi[3][4];       // ... max (rounded up); an empty slot has lo = hi = +inf (never hit)
+    float pnear[3][4];    // slot c's near plane along axis a: pnear[a][c] (rounded outward)
+    int32_t ref[4];       // >= 0: node index within the copy; < 0: ~first TriRec of a reference leaf run
+    float pfar[3][4];     // ... far plane; an empty slot has pnear = pfar = +inf (never hit)
     int32_t pad[4];
 };
 static_assert(sizeof(W4Node) == 128, "W4Node is one 128-B line");
-static_assert(offsetof(W4Node, hi) == offsetof(W4Node, lo) + 64, "near/far rows 64 B apart");
+static_assert(offsetof(W4Node, pfar) == offsetof(W4Node, pnear) + 64, "near/far rows 64 B apart");
 
 struct DMaterial {        // ParsingKit Material fields used by trace()
     double ambient[3], diffuse[3], specular[3], mirror[3], absorption[3];
@@ -237,7 +240,7 @@ struct RenderParams {
     int32_t wide_root;
     double wdelta;
     float weps;
-    int32_t wide_pad;
+    uint32_t wide_copy_bytes;        // bytes of one octant copy of the node array (W4Node)
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

@@ -846,6 +846,7 @@ struct DeviceReplica {
     double* jitter = nullptr;
     FullScratch full;                         // full trace() passes on the replica stream
     void* deep = nullptr; int64_t deep_cap = 0;   // deep trace() frames (render_full<.., true>)
+    std::vector<void*> retired;               // grown scratch's predecessors (retire(), freed at destroy)
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     unsigned long long* wave_times = nullptr; int64_t wave_times_cap = 0;   // rt_debug_wave_times
     hipStream_t stream = nullptr;
@@ -952,8 +953,23 @@ static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
     return RT_OK;
 }
 
+// Scratch grows on demand (a larger chunk selection, a deeper scene), but a grown buffer's
+// predecessor is never freed beside renders in flight: hipFree may wait for the whole device
+// (stalling every in-flight render), and a render still queued on another stream - a caller's
+// stream for rt_render_device, an in-flight slot - may still read it.  It is retired instead and
+// freed with the replica (after a device synchronisation); the new buffer is zeroed, where
+// needed, on the growing render's own stream.  Capacities grow by at least 1.5x, so the retired
+// bytes stay within twice the live scratch.
+static void retire(DeviceReplica& r, void* p) {
+    if (p) r.retired.push_back(p);
+}
+static int64_t grown(int64_t need, int64_t cap) { return std::max(need, cap + cap / 2); }
+
 static void free_replica(DeviceReplica& r) {
     (void)hipSetDevice(r.device);
+    (void)hipDeviceSynchronize();
+    for (void* p : r.retired) (void)hipFree(p);
+    r.retired.clear();
     (void)hipFree(r.wnodes); (void)hipFree(r.lbox);
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
@@ -1190,6 +1206,7 @@ static double dist_to_center(const HostScene& S, const double p[3]) {
 static void set_wide(const HostScene& S, const DeviceReplica& r, RenderParams& P, double origin_coord, bool on,
                      int64_t scale_permille) {
     P.wnodes = r.wnodes; P.lbox = r.lbox; P.wide_root = S.wide_root;
+    P.wide_copy_bytes = (uint32_t)(S.wide_copy * (int64_t)sizeof(W4Node));
     const double R = std::max(S.wide_coord, origin_coord) + std::fabs(S.shadow_eps) + std::fabs(S.eps);
     P.wdelta = R * 0x1p-21 * ((double)scale_permille * 1e-3);
     float we = (float)S.eps;
@@ -1310,7 +1327,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         batch = (int32_t)std::max(1.0, std::min((double)P.num_chunks, std::floor(deep_cap(s) / per_chunk)));
         const int64_t need = (int64_t)(per_chunk * batch);
         if (need > r.deep_cap) {
-            (void)hipFree(r.deep);
+            retire(r, r.deep);
             r.deep = nullptr; r.deep_cap = 0;
             if (hipMalloc(&r.deep, need) != hipSuccess) return fail(RT_ERR_OOM, "device allocation of deep trace() frames failed");
             r.deep_cap = need;
@@ -1333,16 +1350,17 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
     if (alights || (dielectric && !count && !deep)) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
         if (px > fs.cap_px) {
-            (void)hipFree(fs.events); (void)hipFree(fs.jstart);
+            const int64_t cap = grown(px, fs.cap_px);
+            retire(r, fs.events); retire(r, fs.jstart);
             fs.events = nullptr; fs.jstart = nullptr; fs.cap_px = 0;
-            if (hipMalloc((void**)&fs.events, px * sizeof(long long)) != hipSuccess ||
-                hipMalloc((void**)&fs.jstart, px * sizeof(long long)) != hipSuccess) {
-                (void)hipFree(fs.events); (void)hipFree(fs.jstart);
+            if (hipMalloc((void**)&fs.events, cap * sizeof(long long)) != hipSuccess ||
+                hipMalloc((void**)&fs.jstart, cap * sizeof(long long)) != hipSuccess) {
+                (void)hipFree(fs.events); (void)hipFree(fs.jstart);      // never used: safe to free
                 fs.events = nullptr; fs.jstart = nullptr;
                 if (alights) return fail(RT_ERR_OOM, "device allocation of area-light jitter buffers failed");
                 (void)hipGetLastError();
             } else {
-                fs.cap_px = px;
+                fs.cap_px = cap;
             }
         }
         P.events = fs.events;
@@ -1352,7 +1370,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         const int64_t hl = s->opt[kOptHitlog];
         const int64_t slots = count ? 0 : (hl >= 0 ? hl : hit_slots_for(P, dielectric, px));
         if (slots > 0 && slots * px > fs.hitlog_cap) {
-            (void)hipFree(fs.hitlog);
+            retire(r, fs.hitlog);
             fs.hitlog = nullptr; fs.hitlog_cap = 0;
             if (hipMalloc((void**)&fs.hitlog, (size_t)(slots * px) * sizeof(DHitRec)) == hipSuccess) fs.hitlog_cap = slots * px;
             else (void)hipGetLastError();             // no log: render_full walks every ray
@@ -1367,7 +1385,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         bool nodeshade = log && s->opt[kOptNodeshade] != 0;
         if (nodeshade && (slots * px > fs.nodes_cap || px > fs.walks_cap)) {
             const int64_t recs = std::max(slots * px, fs.nodes_cap), pxs = std::max(px, fs.walks_cap);
-            (void)hipFree(fs.nodes); (void)hipFree(fs.node_lo); (void)hipFree(fs.walks);
+            retire(r, fs.nodes); retire(r, fs.node_lo); retire(r, fs.walks);
             fs.nodes = nullptr; fs.node_lo = nullptr; fs.walks = nullptr; fs.nodes_cap = fs.walks_cap = 0;
             if (hipMalloc((void**)&fs.nodes, (size_t)recs * sizeof(DNodeRec)) == hipSuccess &&
                 hipMalloc((void**)&fs.node_lo, (size_t)recs * 3 * sizeof(double)) == hipSuccess &&
@@ -1376,6 +1394,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
                 fs.walks_cap = pxs;
             } else {
                 (void)hipGetLastError();              // render_full shades every hit
+                retire(r, fs.nodes); retire(r, fs.node_lo); retire(r, fs.walks);
+                fs.nodes = nullptr; fs.node_lo = nullptr; fs.walks = nullptr;
             }
         }
         nodeshade = nodeshade && slots * px <= fs.nodes_cap && px <= fs.walks_cap;
@@ -1392,7 +1412,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         bool levels = nodeshade && !deep && P.has_tlas && tree_size > 0 && slots == tree_size * traced &&
                       !rough && s->opt[kOptLevels] != 0;
         if (levels && slots * px > fs.nflags_cap) {
-            (void)hipFree(fs.nflags);
+            retire(r, fs.nflags);
             fs.nflags = nullptr; fs.nflags_cap = 0;
             if (hipMalloc((void**)&fs.nflags, (size_t)(slots * px)) == hipSuccess) fs.nflags_cap = slots * px;
             else (void)hipGetLastError();             // depth-first k_events
@@ -1471,7 +1491,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
 // pixels trace one sample (Int(sqrt(spp)) == 1) with maxRecursionDepth <= kMaxQueueLevels;
 // `arena` grows to levels x (tiles x 64) records, the tile masks and k_qscan's tile list
 // (false: allocation refused or failed -> the bounce megakernel).
-static bool queue_arena(const rt_scene* s, BounceArena* arena, RenderParams& P, int64_t tiles, hipStream_t stream) {
+static bool queue_arena(const rt_scene* s, DeviceReplica& r, BounceArena* arena, RenderParams& P, int64_t tiles,
+                        hipStream_t stream) {
     if (!arena || s->opt[kOptQueue] == 0) return false;
     if (P.cam.n != 1 || P.max_depth < 1 || P.max_depth > kMaxQueueLevels) return false;
     const int64_t levels = P.max_depth;
@@ -1483,9 +1504,11 @@ static bool queue_arena(const rt_scene* s, BounceArena* arena, RenderParams& P, 
                (size_t)((tl + dev::kQScanTiles - 1) / dev::kQScanTiles) * sizeof(unsigned long long);
     };
     if (levels > arena->levels || tiles > arena->tiles) {
-        const int64_t lv = std::max(levels, arena->levels), tl = std::max(tiles, arena->tiles);
+        const int64_t lv = std::max(levels, arena->levels);
+        int64_t tl = tiles > arena->tiles ? grown(tiles, arena->tiles) : arena->tiles;
+        if ((int64_t)bytes(lv, tl) > kQueueBytesCap) tl = std::max(tiles, arena->tiles);
         if ((int64_t)bytes(lv, tl) > kQueueBytesCap) return false;
-        (void)hipFree(arena->base);
+        retire(r, arena->base);
         arena->base = nullptr;
         arena->levels = arena->tiles = 0;
         // zeroed on the render's own stream: a plain hipMemset runs on the null stream, which does
@@ -1539,7 +1562,7 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
         else M_(dev::kWalkGeneral);                                         \
     } while (0)
-    if (bounce && !count && queue_arena(s, arena, P, (int64_t)grid.x * (bt / 64), stream)) {
+    if (bounce && !count && queue_arena(s, r, arena, P, (int64_t)grid.x * (bt / 64), stream)) {
         // primary + shadow rays of every pixel in the spill-free primary instantiation, then per
         // level the tile list (k_qscan) and the level's rays in coherent batches (k_bounce)
 #define MYRT_QPRIM(W_) hipLaunchKernelGGL((dev::render_kernel<false, false, W_, true>), grid, block, lds, stream, P)
@@ -1870,7 +1893,7 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         if (dma) {
             const int64_t px = (int64_t)nq * 8 * W;
             if (px > f.stage_px) {
-                (void)hipFree(f.stage_rgb); (void)hipFree(f.stage_rgba);
+                retire(r, f.stage_rgb); retire(r, f.stage_rgba);
                 f.stage_rgb = nullptr; f.stage_rgba = nullptr; f.stage_px = 0;
                 HIP_TRY(hipMalloc((void**)&f.stage_rgb, px * 3 * sizeof(double)));
                 HIP_TRY(hipMalloc((void**)&f.stage_rgba, px * 4));
@@ -2108,7 +2131,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
         HIP_TRY(hipSetDevice(r.device));
         const int64_t px = (int64_t)pl.rows * W;
         if (!zerocopy && px > r.out_cap_px) {
-            (void)hipFree(r.out_d); (void)hipFree(r.out8_d); r.out_d = nullptr; r.out8_d = nullptr; r.out_cap_px = 0;
+            retire(r, r.out_d); retire(r, r.out8_d); r.out_d = nullptr; r.out8_d = nullptr; r.out_cap_px = 0;
             HIP_TRY(hipMalloc((void**)&r.out_d, px * 3 * sizeof(double)));
             HIP_TRY(hipMalloc((void**)&r.out8_d, px * 4));
             r.out_cap_px = px;

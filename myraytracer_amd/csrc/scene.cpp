@@ -577,17 +577,17 @@ struct WideBuilder {
                 refs[i] = build(c[i]);                   // preorder: children follow their parent
             }
         }
-        W4Node& n = S.wnodes[idx];
+        W4Node& n = S.wnodes[idx];                       // octant 0's copy: near = lo, far = hi
         std::memset(&n, 0, sizeof(n));
         for (int s = 0; s < 4; ++s) {
             for (int k = 0; k < 3; ++k) {
                 if (s < (int)c.size()) {
-                    n.lo[k][s] = down(c[s].lo[k]);
-                    n.hi[k][s] = up(c[s].hi[k]);
+                    n.pnear[k][s] = down(c[s].lo[k]);
+                    n.pfar[k][s] = up(c[s].hi[k]);
                     S.wide_coord = std::fmax(S.wide_coord, std::fmax(std::fabs(c[s].lo[k]), std::fabs(c[s].hi[k])));
                 } else {
-                    n.lo[k][s] = HUGE_VALF;              // empty slot: never hit (wide.h)
-                    n.hi[k][s] = HUGE_VALF;
+                    n.pnear[k][s] = HUGE_VALF;           // empty slot: never hit (wide.h)
+                    n.pfar[k][s] = HUGE_VALF;
                 }
             }
             n.ref[s] = refs[s];
@@ -597,6 +597,57 @@ struct WideBuilder {
     }
 };
 }  // namespace
+
+// The eight octant copies of the four-wide tree (layout.h W4Node).  Copy o (bit a set: rays with
+// d[a] < 0) holds each node with the rows of that octant's near planes first (the box maximum
+// along a when d[a] < 0) and its slots sorted front to back for such rays: by the projection of
+// each slot box's centre on the octant's diagonal (+-1, +-1, +-1), empty slots last, ties in
+// slot order (measured on C3: centres 8,700 Mrays/s, near corners 8,567, slot order 6,105;
+// profiles/r05b_ab_c3.txt).  The walk then continues with the first slot hit and pushes the others in reverse
+// (wide.h), which replaces the per-node distance sort.  Exactness does not depend on the order
+// (wide.h header: only equal-t candidates depend on it, and those are re-walked in the
+// reference's order).  MYRT_WIDE_ORDER (host build, measurement): 1 = near corners instead of
+// centres, 2 = slot order kept.
+static void wide_octant_copies(HostScene& S) {
+    const size_t N = S.wnodes.size();
+    const char* env = std::getenv("MYRT_WIDE_ORDER");
+    const int mode = env ? std::atoi(env) : 0;
+    std::vector<W4Node> out(8 * N);
+    const std::vector<W4Node>& in = S.wnodes;
+    run_chunks(std::min(8, build_threads()), [&](int k) {
+        const int T = std::min(8, build_threads());
+        for (size_t x = (size_t)k; x < 8 * N; x += (size_t)T) {
+            const int o = (int)(x / N);
+            const W4Node& a = in[x % N];
+            W4Node& w = out[x];
+            std::memset(&w, 0, sizeof(w));
+            double key[4];
+            int perm[4] = {0, 1, 2, 3};
+            for (int c = 0; c < 4; ++c) {
+                if (!(a.pnear[0][c] < HUGE_VALF)) { key[c] = HUGE_VAL; continue; }
+                double k = 0.0;
+                for (int ax = 0; ax < 3; ++ax) {
+                    const bool neg = (o >> ax) & 1;
+                    const double lo = a.pnear[ax][c], hi = a.pfar[ax][c];
+                    k += mode == 1 ? (neg ? -hi : lo) : (neg ? -0.5 : 0.5) * (lo + hi);
+                }
+                key[c] = mode == 2 ? (double)c : k;
+            }
+            std::stable_sort(perm, perm + 4, [&](int p, int q) { return key[p] < key[q]; });
+            for (int i = 0; i < 4; ++i) {
+                const int c = perm[i];
+                for (int ax = 0; ax < 3; ++ax) {
+                    const bool neg = (o >> ax) & 1;
+                    w.pnear[ax][i] = neg ? a.pfar[ax][c] : a.pnear[ax][c];
+                    w.pfar[ax][i] = neg ? a.pnear[ax][c] : a.pfar[ax][c];
+                }
+                w.ref[i] = a.ref[c];
+            }
+        }
+    });
+    S.wnodes.swap(out);
+    S.wide_copy = (int64_t)N;
+}
 
 static void build_wide(HostScene& S) {
     S.wnodes.clear();
@@ -621,10 +672,13 @@ static void build_wide(HostScene& S) {
     // a walk holds at most three deferred slots per wide level on its path (plus slack): it must
     // fit the device stack (device.h Stack, kStackCap), else the binary walk
     // (and the walk addresses nodes by 32-bit byte offsets: the array must stay below 4 GB)
+    // (the eight octant copies included)
     if (!std::isfinite(S.wide_coord) || 3 * (int64_t)B.max_depth + 2 > kStackCap ||
-        S.wnodes.size() * sizeof(W4Node) >= (size_t(1) << 32)) {
+        8 * S.wnodes.size() * sizeof(W4Node) >= (size_t(1) << 32)) {
         S.wnodes.clear(); S.lbox.clear(); S.wide_root = -1;
+        return;
     }
+    wide_octant_copies(S);
 }
 
 int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err) {

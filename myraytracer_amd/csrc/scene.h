@@ -80,6 +80,7 @@ struct HostScene {
     std::vector<double> lbox;              // 6 per TriRec index: exact box of the leaf run starting there
     int64_t wide_leaves = 0;               // reference leaves under the wide tree
     int32_t wide_root = -1;                // -1: no wide tree
+    int64_t wide_copy = 0;                 // nodes per octant copy (wnodes holds eight, layout.h W4Node)
     double wide_coord = 0.0;               // largest |coordinate| of any box (wdelta scale)
     // ---- bookkeeping / debug
     int64_t n_meshes = 0, n_tris = 0, n_spheres = 0, n_planes = 0;

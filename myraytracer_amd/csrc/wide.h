@@ -31,15 +31,20 @@
 namespace myrt {
 namespace dev {
 
-// The ray in the walk's FP32 form.  Per axis the near plane of every box is lo when 1/d >= 0 and
-// hi otherwise: the walk reads each slot's near and far planes directly (a per-lane byte offset
-// into the node, nx/ny/nz) instead of taking min/max of both plane distances - the same values
-// (FMA is monotone, and the lo-plane offset is below the hi-plane one), 24 VALU fewer per node.
+// The ray in the walk's FP32 form.  The node array holds one copy of the tree per direction
+// octant (layout.h W4Node): in the copy of the ray's octant every node's rows are already its
+// near planes (the box minimum along a when d[a] >= 0, the maximum otherwise) and far planes, so a
+// slot's entry distance is max3 of three FMAs on the near row and its exit min3 on the far row -
+// the same values as min/max of both plane distances (FMA is monotone, and the lo-plane offset is
+// below the hi-plane one) - and its slots are in front-to-back order for that octant.
+typedef float wf2 __attribute__((ext_vector_type(2)));
+typedef float wf4 __attribute__((ext_vector_type(4)));
+typedef int wi4 __attribute__((ext_vector_type(4)));
 struct WRay {
     float ix, iy, iz;     // 1/d in FP32
     float nox, noy, noz;  // offset of the near planes: -(o/d) - wdelta*|1/d|
     float fox, foy, foz;  // offset of the far planes:  -(o/d) + wdelta*|1/d|
-    unsigned nx, ny, nz;  // byte offset of the near-plane row of axis a in a W4Node (lo or hi)
+    unsigned obase;       // byte offset of this octant's copy of the node array
     bool uoct;            // every lane of the wave has this direction octant (wave-uniform)
 };
 
@@ -56,11 +61,8 @@ __device__ __forceinline__ WRay wide_ray(const RenderParams& P, const V3& o, con
     const double dx = P.wdelta * fabs(inv.x), dy = P.wdelta * fabs(inv.y), dz = P.wdelta * fabs(inv.z);
     r.nox = (float)(-ox - dx); r.noy = (float)(-oy - dy); r.noz = (float)(-oz - dz);
     r.fox = (float)(-ox + dx); r.foy = (float)(-oy + dy); r.foz = (float)(-oz + dz);
-    constexpr unsigned kHi = offsetof(W4Node, hi);        // 64: hi row a = lo row a + 64 B
-    r.nx = (inv.x >= 0 ? 0u : kHi) + 0u * 16u;
-    r.ny = (inv.y >= 0 ? 0u : kHi) + 1u * 16u;
-    r.nz = (inv.z >= 0 ? 0u : kHi) + 2u * 16u;
-    const unsigned oct = r.nx | (r.ny << 8) | (r.nz << 16);
+    const unsigned oct = (inv.x >= 0 ? 0u : 1u) | (inv.y >= 0 ? 0u : 2u) | (inv.z >= 0 ? 0u : 4u);
+    r.obase = oct * P.wide_copy_bytes;
     r.uoct = __all(oct == (unsigned)__builtin_amdgcn_readfirstlane((int)oct));
     return r;
 }
@@ -75,146 +77,86 @@ __device__ __forceinline__ unsigned long long wide_entry(int ref, float t) {
     return (unsigned long long)(unsigned)ref | ((unsigned long long)__float_as_uint(t) << 32);
 }
 
-// One four-wide node: the slots whose widened box the ray enters within [weps, lim].  Closest
-// hit: continue with the nearest entry, the others are pushed; any hit: continue with the first
-// slot hit (the reference's occludedBLAS takes L first, RTContext.swift:823-825).  Returns false
+// One four-wide node: the slots whose widened box the ray enters within [weps, lim].  The walk
+// continues with the first slot hit in the node's (octant) order and pushes the others last
+// first, so they pop in that order; for any-hit walks the order is immaterial.  Returns false
 // when no slot is hit (the caller pops).
-#ifndef MYRT_MT_TWICE
-#define MYRT_MT_TWICE 0
-#endif
-typedef float wf4 __attribute__((ext_vector_type(4)));
-typedef int wi4 __attribute__((ext_vector_type(4)));
-#ifndef MYRT_WIDE_SCALAR
-#define MYRT_WIDE_SCALAR 1
-#endif
-template <bool SHADOW>
+template <class RowF4, class RowI4>
 __device__ __forceinline__ bool wide_node(const RenderParams& P, int& ref, const WRay& R, float lim, Stack& st,
-                                          const wf4& nx, const wf4& fx, const wf4& ny, const wf4& fy, const wf4& nz,
-                                          const wf4& fz, const wi4& refs);
-template <bool SHADOW>
+                                          RowF4 row, RowI4 refrow) {
+    constexpr unsigned kFar = offsetof(W4Node, pfar), kRef = offsetof(W4Node, ref);
+    const wf4 nx = row(0u), ny = row(16u), nz = row(32u);
+    const wf4 fx = row(kFar), fy = row(kFar + 16u), fz = row(kFar + 32u);
+    const wi4 refs = refrow(kRef);
+    // the 24 plane distances (FP32 FMAs; packed v_pk_fma_f32 forms measured slower: their splat
+    // register pairs spilled, and the op_sel inline-asm form lost the loads' latency overlap,
+    // profiles/r05c_ab_c3.txt)
+    auto fm = [](wf2 a, float b, float c) { return wf2{__builtin_fmaf(a.x, b, c), __builtin_fmaf(a.y, b, c)}; };
+    const wf2 anx0 = fm(nx.xy, R.ix, R.nox), anx1 = fm(nx.zw, R.ix, R.nox);
+    const wf2 any0 = fm(ny.xy, R.iy, R.noy), any1 = fm(ny.zw, R.iy, R.noy);
+    const wf2 anz0 = fm(nz.xy, R.iz, R.noz), anz1 = fm(nz.zw, R.iz, R.noz);
+    const wf2 afx0 = fm(fx.xy, R.ix, R.fox), afx1 = fm(fx.zw, R.ix, R.fox);
+    const wf2 afy0 = fm(fy.xy, R.iy, R.foy), afy1 = fm(fy.zw, R.iy, R.foy);
+    const wf2 afz0 = fm(fz.xy, R.iz, R.foz), afz1 = fm(fz.zw, R.iz, R.foz);
+    const float tn[4] = {__builtin_fmaxf(__builtin_fmaxf(anx0.x, any0.x), anz0.x),
+                         __builtin_fmaxf(__builtin_fmaxf(anx0.y, any0.y), anz0.y),
+                         __builtin_fmaxf(__builtin_fmaxf(anx1.x, any1.x), anz1.x),
+                         __builtin_fmaxf(__builtin_fmaxf(anx1.y, any1.y), anz1.y)};
+    const float tf[4] = {__builtin_fminf(__builtin_fminf(afx0.x, afy0.x), afz0.x),
+                         __builtin_fminf(__builtin_fminf(afx0.y, afy0.y), afz0.y),
+                         __builtin_fminf(__builtin_fminf(afx1.x, afy1.x), afz1.x),
+                         __builtin_fminf(__builtin_fminf(afx1.y, afy1.y), afz1.y)};
+    const int nr[4] = {refs.x, refs.y, refs.z, refs.w};
+    bool h[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) h[c] = __builtin_fmaxf(tn[c], P.weps) <= __builtin_fminf(tf[c], lim);
+    // continue with the first slot hit; keep the later hits (they all come after it)
+    const int nref = h[0] ? nr[0] : h[1] ? nr[1] : h[2] ? nr[2] : nr[3];
+    const bool keep[4] = {false, h[1] && h[0], h[2] && (h[0] || h[1]), h[3] && (h[0] || h[1] || h[2])};
+    if (!__any(st.sp > kLds - 3)) {
+        // every lane's three candidate entries lie in LDS: unconditional stores at running
+        // positions (a dropped entry is overwritten by the next kept one, or lies above the top)
+        int p = st.sp;
+#pragma unroll
+        for (int c = 3; c >= 1; --c) {
+            st.lds[p * Stack::stride] = wide_entry(nr[c], tn[c]);
+            p += keep[c] ? 1 : 0;
+        }
+        st.sp = p;
+    } else {
+#pragma unroll
+        for (int c = 3; c >= 1; --c) st.push_raw_if(keep[c], wide_entry(nr[c], tn[c]));
+    }
+    ref = nref;
+    return h[0] || h[1] || h[2] || h[3];
+}
+
+// One node step: the rows of node `ref` in this ray's octant copy (base = P.wnodes).
 __device__ __forceinline__ bool wide_inner(const RenderParams& P, const char* base, int& ref, const WRay& R, float lim,
                                            Stack& st) {
-    // near / far plane rows of this lane's direction octant (the far row of axis a is the other of
-    // lo[a] / hi[a], 64 B away: offset n ^ 64); base = P.wnodes
-    constexpr unsigned kHi = offsetof(W4Node, hi);
-    if (MYRT_WIDE_SCALAR && R.uoct) {
+    if (R.uoct) {
         // Every lane at the same node with the same octant (the top of the tree for a tile's
         // coherent rays): the rows come through the scalar cache into SGPRs once for the wave,
         // instead of 64 copies through the vector-memory data path (TD, ~0.87 busy).
         const int r0 = __builtin_amdgcn_readfirstlane(ref);
         if (__all(ref == r0)) {
-            const unsigned long long av = (unsigned long long)(base + (size_t)r0 * sizeof(W4Node));
+            const unsigned nb = __builtin_amdgcn_readfirstlane(R.obase) + (unsigned)r0 * (unsigned)sizeof(W4Node);
+            const unsigned long long av = (unsigned long long)(base + (size_t)nb);
             const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
             const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
             typedef const __attribute__((address_space(4))) char c4_char;
             c4_char* sb = (c4_char*)((unsigned long long)alo | ((unsigned long long)ahi << 32));
             typedef const __attribute__((address_space(4))) wf4 c4_f4;
             typedef const __attribute__((address_space(4))) wi4 c4_i4;
-            const unsigned ox = __builtin_amdgcn_readfirstlane(R.nx), oy = __builtin_amdgcn_readfirstlane(R.ny),
-                           oz = __builtin_amdgcn_readfirstlane(R.nz);
-            const wf4 nx = *(c4_f4*)(sb + ox), fx = *(c4_f4*)(sb + (ox ^ kHi));
-            const wf4 ny = *(c4_f4*)(sb + oy), fy = *(c4_f4*)(sb + (oy ^ kHi));
-            const wf4 nz = *(c4_f4*)(sb + oz), fz = *(c4_f4*)(sb + (oz ^ kHi));
-            const wi4 refs = *(c4_i4*)(sb + offsetof(W4Node, ref));
-            return wide_node<SHADOW>(P, ref, R, lim, st, nx, fx, ny, fy, nz, fz, refs);
+            return wide_node(P, ref, R, lim, st, [&](unsigned off) { return *(c4_f4*)(sb + off); },
+                             [&](unsigned off) { return *(c4_i4*)(sb + off); });
         }
     }
-    // 32-bit byte offsets from the array base (the host keeps the node array below 4 GB): the loads
-    // take the SGPR-base + VGPR-offset form instead of a 64-bit address add per row
-    const unsigned nb = (unsigned)ref * (unsigned)sizeof(W4Node);
-    auto row = [&](unsigned off) { return *reinterpret_cast<const wf4*>(base + (size_t)(nb + off)); };
-    const wf4 nx = row(R.nx), fx = row(R.nx ^ kHi);
-    const wf4 ny = row(R.ny), fy = row(R.ny ^ kHi);
-    const wf4 nz = row(R.nz), fz = row(R.nz ^ kHi);
-    const wi4 refs = *reinterpret_cast<const wi4*>(base + (size_t)(nb + (unsigned)offsetof(W4Node, ref)));
-    return wide_node<SHADOW>(P, ref, R, lim, st, nx, fx, ny, fy, nz, fz, refs);
-}
-
-// The slab tests of one node's four slots and the stack update (wide_inner).
-template <bool SHADOW>
-__device__ __forceinline__ bool wide_node(const RenderParams& P, int& ref, const WRay& R, float lim, Stack& st,
-                                          const wf4& nx, const wf4& fx, const wf4& ny, const wf4& fy, const wf4& nz,
-                                          const wf4& fz, const wi4& refs) {
-    const int nr[4] = {refs.x, refs.y, refs.z, refs.w};
-    float a[4];
-    bool h[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nx[c], R.ix, R.nox), __builtin_fmaf(ny[c], R.iy, R.noy)),
-                                         __builtin_fmaf(nz[c], R.iz, R.noz));
-        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaf(fx[c], R.ix, R.fox), __builtin_fmaf(fy[c], R.iy, R.foy)),
-                                         __builtin_fmaf(fz[c], R.iz, R.foz));
-        a[c] = tn;
-        h[c] = __builtin_fmaxf(tn, P.weps) <= __builtin_fminf(tf, lim);
-    }
-#ifndef MYRT_WIDE_SORT
-#define MYRT_WIDE_SORT 1
-#endif
-    if ((!SHADOW && MYRT_WIDE_SORT) || (SHADOW && MYRT_WIDE_SORT >= 2)) {
-        // closest hit (and, at MYRT_WIDE_SORT 2, any hit), full front-to-back order: sort the four
-        // (entry, ref) pairs (5 compare-exchanges), continue with the nearest, push the others far
-        // to near
-        float k[4];
-        int r[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) { k[c] = h[c] ? a[c] : __builtin_inff(); r[c] = nr[c]; }
-        auto ce = [&](int i, int j) {
-            const bool sw = k[j] < k[i];
-            const float ki = sw ? k[j] : k[i], kj = sw ? k[i] : k[j];
-            const int ri = sw ? r[j] : r[i], rj = sw ? r[i] : r[j];
-            k[i] = ki; k[j] = kj; r[i] = ri; r[j] = rj;
-        };
-        ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-        if (!__any(st.sp > kLds - 4)) {
-            int p = st.sp;
-#pragma unroll
-            for (int c = 3; c >= 1; --c) {
-                st.lds[p * Stack::stride] = wide_entry(r[c], k[c]);
-                p += k[c] < __builtin_inff() ? 1 : 0;
-            }
-            st.sp = p;
-        } else {
-#pragma unroll
-            for (int c = 3; c >= 1; --c) st.push_raw_if(k[c] < __builtin_inff(), wide_entry(r[c], k[c]));
-        }
-        ref = r[0];
-        return k[0] < __builtin_inff();
-    }
-    int n;          // the slot the walk continues with
-    int nref;
-    if (SHADOW) {
-        n = h[0] ? 0 : h[1] ? 1 : h[2] ? 2 : 3;
-        nref = h[0] ? nr[0] : h[1] ? nr[1] : h[2] ? nr[2] : nr[3];
-    } else {
-        const float k0 = h[0] ? a[0] : __builtin_inff(), k1 = h[1] ? a[1] : __builtin_inff();
-        const float k2 = h[2] ? a[2] : __builtin_inff(), k3 = h[3] ? a[3] : __builtin_inff();
-        const bool p = k1 < k0, q = k3 < k2;
-        const float m01 = p ? k1 : k0, m23 = q ? k3 : k2;
-        const int r01 = p ? nr[1] : nr[0], r23 = q ? nr[3] : nr[2];
-        const bool z = m23 < m01;
-        nref = z ? r23 : r01;
-        n = z ? (q ? 3 : 2) : (p ? 1 : 0);
-    }
-    // the others, last slot first (they pop in slot order)
-    bool keep[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) keep[c] = h[c] && c != n;
-    if (!__any(st.sp > kLds - 4)) {
-        // every lane's four candidate slots lie in LDS: unconditional stores at running positions
-        // (a dropped entry is overwritten by the next kept one, or lies above the new top)
-        int p = st.sp;
-#pragma unroll
-        for (int c = 3; c >= 0; --c) {
-            st.lds[p * Stack::stride] = wide_entry(nr[c], a[c]);
-            p += keep[c] ? 1 : 0;
-        }
-        st.sp = p;
-    } else {
-#pragma unroll
-        for (int c = 3; c >= 0; --c) st.push_raw_if(keep[c], wide_entry(nr[c], a[c]));
-    }
-    ref = nref;
-    return h[0] || h[1] || h[2] || h[3];
+    // 32-bit byte offsets from the array base (the host keeps the array below 4 GB): the loads
+    // take the SGPR-base + VGPR-offset + immediate form, one address per node
+    const unsigned nb = R.obase + (unsigned)ref * (unsigned)sizeof(W4Node);
+    return wide_node(P, ref, R, lim, st, [&](unsigned off) { return *reinterpret_cast<const wf4*>(base + (size_t)nb + off); },
+                     [&](unsigned off) { return *reinterpret_cast<const wi4*>(base + (size_t)nb + off); });
 }
 
 // next entry whose (FP32, <= FP64) entry distance does not exceed lim
@@ -288,7 +230,7 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
             if (in) c.recs++;
         }
         if (ref >= 0) {
-            if (wide_inner<SHADOW>(P, wbase, ref, R, lim, st)) continue;
+            if (wide_inner(P, wbase, ref, R, lim, st)) continue;
         } else {
             const int t0 = ~ref;
             int box = 0;                                   // leaf box: 0 unchecked, 1 passes, 2 fails
@@ -297,27 +239,12 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
                     const auto T = tris[t];                // by value: `last` arrives with the vertices
                     if (COUNT) c.tris++;
                     if (SHADOW) {
-#if MYRT_MT_TWICE   // measurement variant: every triangle test runs twice (the difference prices the tests)
-                        {
-                            V3 o2 = o;
-                            asm volatile("" : "+v"(o2.x));
-                            if (tri_shadow(T, o2, d, 0.0, tmax, eps, P.fast_rcp)) asm volatile("" ::: "memory");
-                        }
-#endif
                         if (tri_shadow(T, o, d, 0.0, tmax, eps, P.fast_rcp)) {
                             if (box == 0) box = leaf_box_exact(P, t0, o, d) ? 1 : 2;
                             if (box == 1) return true;
                         }
                     } else {
                         double tt, uu, vv;
-#if MYRT_MT_TWICE
-                        {
-                            V3 o2 = o;
-                            asm volatile("" : "+v"(o2.x));
-                            double t2, u2, v2;
-                            if (tri_candidate(T, o2, d, tlo, eps, h.t, t2, u2, v2, P.fast_rcp)) asm volatile("" ::: "memory");
-                        }
-#endif
                         const int r = tri_candidate(T, o, d, tlo, eps, h.t, tt, uu, vv, P.fast_rcp);
                         if (r != 0) {
                             if (box == 0) box = leaf_box_exact(P, t0, o, d) ? 1 : 2;

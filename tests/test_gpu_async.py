@@ -234,3 +234,58 @@ def test_pipelined_mirror_frames_against_the_oracle(queue):
         eng.wait(t)
         assert np.array_equal(fbs[kk % Q], ref8)
     eng.close()
+
+
+def _chunk_rows(H, first, step):
+    rows = np.zeros(H, bool)
+    for c in range(first, (H + 7) // 8, step):
+        rows[8 * c: 8 * c + 8] = True
+    return rows
+
+
+def test_scratch_growth_beside_renders_in_flight():
+    """Scratch grows while other renders are in flight (the race class of round 4's
+    undelivered mirror pixels): the compacted bounce render's queues of every in-flight slot grow
+    three times (a quarter, half, then all of the chunks) while the other slots' renders run, and
+    two device renders on one stream grow the device path's queues back to back with no host
+    synchronisation between them.  Grown buffers' predecessors are retired, not freed, and the new
+    ones are zeroed on the growing render's stream (render.hip retire / queue_arena).  Every frame
+    equals the oracle on its selected rows."""
+    import torch
+    from test_gpu_features import _mirror_corridor
+    sc = _mirror_corridor(4, 96, 64)
+    W, H = 96, 64
+    ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
+    eng = M.RayTracerEngine(sc)
+    assert eng.get_option("queue") == 1
+    Q = A.RT_MAX_IN_FLIGHT
+    sels = [(k % 4, 4) for k in range(Q)] + [(k % 2, 2) for k in range(Q)] + [(0, 1)] * (Q + 3)
+    fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
+    pend = []
+
+    def check(kk, t):
+        eng.wait(t)
+        rows = _chunk_rows(H, *sels[kk])
+        got = fbs[kk % Q]
+        assert np.array_equal(got[rows], ref8[rows]), f"frame {kk} (chunks {sels[kk]}) differs"
+        assert not got[~rows].any()
+
+    for k, (first, step) in enumerate(sels):
+        if len(pend) == Q:
+            check(*pend.pop(0))
+        fbs[k % Q].fill(0)
+        pend.append((k, eng.submit_into(0, first, step, rgba=fbs[k % Q], frame_layout=True)))
+    for kk, t in pend:
+        check(kk, t)
+    # device path: two renders on one stream, the second growing the queues the first still uses
+    s = torch.cuda.Stream()
+    small = torch.full((H // 4 + 8, W, 3), -1.0, dtype=torch.float64, device="cuda")
+    full = torch.full((H, W, 3), -1.0, dtype=torch.float64, device="cuda")
+    eng.render_device(small.data_ptr(), 0, 1, 4, stream=s.cuda_stream)
+    eng.render_device(full.data_ptr(), 0, 0, 1, stream=s.cuda_stream)
+    s.synchronize()
+    assert float(np.abs(full.cpu().numpy() - ref).max()) <= 1e-5
+    rows = _chunk_rows(H, 1, 4)
+    assert float(np.abs(small.cpu().numpy()[: rows.sum()] - ref[rows]).max()) <= 1e-5
+    assert eng.info().scratch_bytes > 0
+    eng.close()

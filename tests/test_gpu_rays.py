@@ -255,6 +255,27 @@ def test_equal_t_ties_between_instances(walk):
         assert st.rewalked == 0
 
 
+@pytest.mark.parametrize("variant", ["area_light", "glass"])
+def test_equal_t_ties_in_the_full_trace_passes(variant):
+    """The twin-mesh ties through the full trace() kernels (k_level / k_events walk, k_shade,
+    render_full): an area light (jitterIndex events) or glass on the second twin (dielectric
+    paths).  Frames equal the oracle's and the re-walks are counted (rt_stats.rewalked > 0)."""
+    sc, hp = _twin_meshes()
+    if variant == "area_light":
+        sc.area_lights = [M.AreaLight(position=(0.0, 9.0, 1.0), normal=(0.0, -1.0, 0.1), radiance=(400.0, 380.0, 350.0),
+                                      size=2.0)]
+    else:
+        sc.materials[1] = M.Material(ambient=(0.0, 0.0, 0.0), diffuse=(0.05, 0.05, 0.05), specular=(0.5, 0.5, 0.5),
+                                     phong=60.0, ior=1.5, absorption=(0.02, 0.04, 0.08), type="dielectric")
+        sc.objects[0], sc.objects[1] = sc.objects[1], sc.objects[0]     # the glass twin is visited first
+    eng = _engine(sc, "wide")
+    rgb, rgba, st = eng.render_rows(0, 0, 1, True)
+    ref, ref8, _ = oracle.OracleScene(sc).render(0, 0, 1, threads=0, rgba=True)
+    eng.close()
+    assert float(np.abs(rgb - ref).max()) <= 1e-5 and np.array_equal(rgba, ref8)
+    assert st.rewalked > 0, "ties in the full trace() passes are not counted"
+
+
 def _transformed_instances():
     """Instances of one mesh under scales, rotations and translations - triangles only, nothing
     moving."""
