@@ -83,6 +83,11 @@ def parse():
                         "one shared page-locked framebuffer; staged = rows delivered by each GPU's DMA engine "
                         "into a private page-locked frame, then copied by the rank's host thread into the "
                         "shared frame (no concurrent PCIe stores from 8 GPUs into one segment)")
+    p.add_argument("--numa", default="none", choices=["none", "first-touch"],
+                   help="N > 1 strong, shared gather: first-touch = each rank binds its CPU affinity to its GPU's "
+                        "NUMA node (when the process may run there) and touches its own rows of every shared "
+                        "frame before any rank registers it, so those pages live on its GPU's socket; none = "
+                        "pages land where the first registering process faults them")
     p.add_argument("--in-flight", type=int, default=0,
                    help="renders in flight (rt_render_submit); 1 = one frame at a time; 0 = RT_MAX_IN_FLIGHT (16)")
     p.add_argument("--hw-queues", type=int, default=-1,
@@ -145,6 +150,78 @@ class SharedFrame:
             os.unlink(self.path)
 
 
+def _cpulist(text):
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def _ranges(cpus):
+    cpus = sorted(cpus)
+    out, k = [], 0
+    while k < len(cpus):
+        j = k
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(f"{cpus[k]}-{cpus[j]}" if j > k else str(cpus[k]))
+        k = j + 1
+    return ",".join(out)
+
+
+def numa_nodes():
+    """{node: [cpus]} from sysfs (empty when the machine exposes no NUMA topology)."""
+    base = "/sys/devices/system/node"
+    nodes = {}
+    try:
+        for d in os.listdir(base):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(os.path.join(base, d, "cpulist")) as fh:
+                    nodes[int(d[4:])] = _cpulist(fh.read())
+    except OSError:
+        pass
+    return nodes
+
+
+def gpu_numa_node(dev):
+    """NUMA node of GPU `dev` (its PCI function's numa_node in sysfs), or None."""
+    import torch
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        dom, bus, slot = (int(getattr(pr, "pci_domain_id", 0)), int(getattr(pr, "pci_bus_id")),
+                          int(getattr(pr, "pci_device_id")))
+        path = f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{slot:02x}.0/numa_node"
+        with open(path) as fh:
+            n = int(fh.read().strip())
+        return {"node": n if n >= 0 else None, "pci": f"{dom:04x}:{bus:02x}:{slot:02x}.0"}
+    except Exception as e:  # pragma: no cover - depends on the machine
+        return {"node": None, "error": f"{type(e).__name__}: {e}"}
+
+
+def pages_by_node(addr, nbytes):
+    """{node: pages} of the pages in [addr, addr + nbytes) that are present (move_pages(2) with no
+    target nodes reports each page's node; x86-64 syscall 279).  None where unavailable."""
+    import ctypes
+    if nbytes <= 0:
+        return {}
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        pg = os.sysconf("SC_PAGE_SIZE")
+        first = addr // pg * pg
+        n = (addr + nbytes - first + pg - 1) // pg
+        pages = (ctypes.c_void_p * n)(*[first + k * pg for k in range(n)])
+        status = (ctypes.c_int * n)()
+        if libc.syscall(279, 0, ctypes.c_ulong(n), pages, None, status, 0) != 0:
+            return None
+    except Exception:  # pragma: no cover - depends on the machine
+        return None
+    out = collections.Counter(int(x) for x in status if x >= 0)
+    return {str(k): v for k, v in sorted(out.items())}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +266,18 @@ def main():
     dev_override = os.environ.get("MYRT_BENCH_DEVICE")
     local = int(dev_override) if dev_override is not None else local
     torch.cuda.set_device(local)
+    # NUMA: this rank's GPU node, CPU affinity, and (opt-in) the affinity bound to the GPU's node
+    nodes = numa_nodes()
+    gnode = gpu_numa_node(local)
+    numa = {"gpu": gnode, "placement": args.numa, "affinity_before": _ranges(os.sched_getaffinity(0))}
+    if args.numa == "first-touch" and gnode.get("node") is not None and gnode["node"] in nodes:
+        want = set(nodes[gnode["node"]]) & os.sched_getaffinity(0)
+        if want:
+            os.sched_setaffinity(0, want)
+        numa["bound_to_gpu_node"] = bool(want)
+    aff = os.sched_getaffinity(0)
+    numa["affinity"] = _ranges(aff)
+    numa["affinity_nodes"] = sorted(n for n, c in nodes.items() if aff & set(c))
 
     import myraytracer_amd as M
     from myraytracer_amd import _abi as A
@@ -244,11 +333,19 @@ def main():
     staged = strong and world > 1 and args.gather == "staged"
     my_rows = None
     if strong and world > 1:
+        mine_rows = np.concatenate([np.arange(8 * c, min(8 * c + 8, H)) for c in range(first, (H + 7) // 8, step)])
         for q in range(Q):
             sf = SharedFrame(W * H * 4, rank, world, dist, f"{args.config}{q}")
-            if not staged:
-                M.register_host(sf.array)
             shared.append(sf)
+        if args.numa == "first-touch" and not staged:
+            # every rank first-touches its own rows (8-row chunks c = rank mod world) while bound to
+            # its GPU's node; registration (which faults every page it touches first) waits for all
+            for sf in shared:
+                sf.array.reshape(H, W, 4)[mine_rows] = 0
+            dist.barrier()
+        if not staged:
+            for sf in shared:
+                M.register_host(sf.array)
         gathered = [sf.array.reshape(H, W, 4) for sf in shared]
         if staged:
             # private page-locked frames, written by the DMA engine; the host copies this rank's
@@ -300,6 +397,27 @@ def main():
         return last
 
     st = run(max(1, args.warmup))
+    scratch_after_warmup = int(eng.info().scratch_bytes)
+    # where this rank's rows of the delivered frames live (pages per NUMA node; the shared frames
+    # for N > 1, this rank's own page-locked frames for N = 1)
+    if strong and world > 1 and not staged:
+        pg = collections.Counter()
+        row_b = W * 4
+        for sf in shared:
+            base = sf.array.ctypes.data
+            for c in range(first, (H + 7) // 8, step):
+                got = pages_by_node(base + 8 * c * row_b, min(8, H - 8 * c) * row_b) or {}
+                for k_, v_ in got.items():
+                    pg[k_] += v_
+        numa["frame_pages_by_node"] = dict(pg)
+        numa["frame_pages_what"] = "this rank's rows of the shared frames: pages per NUMA node (move_pages)"
+    else:
+        pg = collections.Counter()
+        for fb_ in fbs:
+            for k_, v_ in (pages_by_node(fb_.ctypes.data, fb_.nbytes) or {}).items():
+                pg[k_] += v_
+        numa["frame_pages_by_node"] = dict(pg)
+        numa["frame_pages_what"] = "this rank's page-locked frames: pages per NUMA node (move_pages)"
     rays_primary = rows * W * n * n
     shadow_cast, shadow_traced = int(st.shadow_rays), int(st.shadow_rays_traced)
     rays_rank = rays_primary + shadow_traced
@@ -350,6 +468,8 @@ def main():
                             dtype=torch.float64)
         allr = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(allr, mine)
+        numa_r = [None] * world
+        dist.all_gather_object(numa_r, numa)
         ms_r = [round(float(x[0]), 4) for x in allr]
         dv_r = [round(float(x[3]), 4) for x in allr]
         per_rank = {"ms_per_step": ms_r, "device_ms_per_frame": dv_r,
@@ -357,6 +477,7 @@ def main():
                     "rows": [int(x[2]) for x in allr], "min_ms": min(ms_r), "max_ms": max(ms_r),
                     "device_max_ms": max(dv_r), "delivery_overhead": round(max(ms_r) / max(1e-9, max(dv_r)), 4),
                     "imbalance": round(max(ms_r) / max(1e-9, min(ms_r)), 4), "gather": args.gather,
+                    "numa": numa_r,
                     "what": "per rank: its own timed-region clock per frame (value uses the max, image delivered "
                             "to the shared host frame), the same pipelined loop with the image left in HBM "
                             f"({n_dev} frames, device_ms_per_frame), host time inside rt_render_submit per "
@@ -431,6 +552,9 @@ def main():
                      "rewalked_what": "closest-hit rays of rank 0's share that the four-wide walk handed to the "
                                       "reference-order walk (two candidates at the final t, wide.h)"},
             "per_rank": per_rank,
+            "numa": numa if world == 1 else {"placement": args.numa, "per_rank": "per_rank.numa"},
+            "scene": {"device_bytes": int(info.device_bytes), "scratch_bytes_after_warmup": scratch_after_warmup,
+                      "build_ms": round(float(info.build_ms), 1), "upload_ms": round(float(info.upload_ms), 1)},
             "timing": {"in_flight": Q, "submit_to_done_ms": round(statistics.mean(calls), 4),
                        "submit_us_per_frame": round(submit_s[0] * 1e6 / args.steps, 2),
                        "one_frame_ms": round(sync_ms, 4), "kernel_ms": round(kernel_ms, 4),

@@ -274,7 +274,12 @@ int32_t rt_host_unregister(void* ptr);
  * once the stream has drained.  Device renders have their own counters, pass scratch and
  * queues, so they may overlap rt_render / rt_render_submit renders of the same scene;
  * exception: scenes with maxRecursionDepth > 16 share one deep-frame buffer per replica,
- * and a device render of such a scene must not overlap another render of it. */
+ * and a device render of such a scene must not overlap another render of it.
+ * Device renders of ONE slot share those counters and scratch among themselves: issue them
+ * on one stream (or order them externally); two concurrent device renders of a slot on
+ * different streams race.  Scratch that grows is never freed under a render still queued
+ * (the old buffer is retired until rt_scene_destroy), and the call itself reads the scene's
+ * options under the scene's lock. */
 int32_t rt_render_device(rt_scene* scene, int32_t device_slot, int32_t camera_index,
                          int32_t chunk_first, int32_t chunk_step,
                          double* d_out_rgb, uint8_t* d_out_rgba8, void* stream);

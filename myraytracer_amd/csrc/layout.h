@@ -84,6 +84,18 @@ struct alignas(128) W4Node {
 static_assert(sizeof(W4Node) == 128, "W4Node is one 128-B line");
 static_assert(offsetof(W4Node, pfar) == offsetof(W4Node, pnear) + 64, "near/far rows 64 B apart");
 
+// Per instance of a transformed scene's four-wide walk (wide.h tw_walk): the exact FP64 box of
+// the TLAS leaf holding the instance (world space: tested when the walk enters the instance,
+// the reference's intersectTLAS leaf test, RTContext.swift:632-646), the largest |coordinate| of
+// its BLAS's boxes (local space: the per-ray widening bound) and its BLAS's four-wide root.
+struct DWideInst {
+    double tbox[6];       // lo x, y, z, hi x, y, z
+    double bcoord;
+    int32_t wroot;        // >= 0 node index, < 0 a single leaf run (~first TriRec)
+    int32_t pad;
+};
+static_assert(sizeof(DWideInst) == 64, "DWideInst is 64 B");
+
 struct DMaterial {        // ParsingKit Material fields used by trace()
     double ambient[3], diffuse[3], specular[3], mirror[3], absorption[3];
     double phong, ior, absorption_index, roughness;
@@ -241,6 +253,12 @@ struct RenderParams {
     double wdelta;
     float weps;
     uint32_t wide_copy_bytes;        // bytes of one octant copy of the node array (W4Node)
+    // transformed scenes' four-wide walk (wide.h tw_walk; wide_root is then the TLAS's root):
+    // nodes [0, tw_tlas_nodes) of each copy are the TLAS's (world space), the rest the BLASes'
+    // (local space); TLAS leaves became instance markers ~(ut_marker_base + instance)
+    const DWideInst* winst;
+    int32_t tw_tlas_nodes;
+    float tw_wscale;                 // the local rays' widening factor (option wide_delta_scale / 1000)
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

@@ -37,6 +37,27 @@ __device__ __forceinline__ unsigned long long pixel_seed(int i, int j) {
     return (((unsigned long long)j << 32) ^ (unsigned long long)i) + 0x9E3779B97F4A7C15ull;
 }
 
+// The reference-order transformed walk as the four-wide transformed walk's fallback (ties, local
+// rays out of its FP32 range): out of line, so its registers do not weigh on the wide walk's.
+#ifndef MYRT_TW_CALL
+#define MYRT_TW_CALL 0
+#endif
+#if MYRT_TW_CALL
+#define MYRT_TW_INLINE __noinline__
+#else
+#define MYRT_TW_INLINE __forceinline__
+#endif
+__device__ MYRT_TW_INLINE void ut_closest_call(const RenderParams& P, const V3 o, const V3 d, const V3 inv, double tlo,
+                                            double time, Hit& h, Stack& st) {
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    (void)ut_walk<false>(P, o, d, inv, tlo, DINF, time, h, st);
+}
+__device__ MYRT_TW_INLINE bool ut_occluded_call(const RenderParams& P, const V3 o, const V3 d, double tmax, double time,
+                                             Stack& st) {
+    Hit hu;
+    return ut_walk<true>(P, o, d, rcp(d), 0.0, tmax, time, hu, st);
+}
+
 // Closest hit of one ray by the scene's walk (WALK, render_kernel).
 template <bool COUNT, int WALK, bool WIDE = true>
 __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
@@ -45,6 +66,17 @@ __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o,
         uni_closest<COUNT, WIDE>(P, o, d, inv, tlo, h, st, c);
     } else if (WALK == kWalkTransformed) {
         h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+        if (WIDE && P.wide && P.winst && __all(wide_ok(inv))) {
+            // the four-wide walk of transformed scenes (wide.h tw_walk); equal-t candidates and
+            // local rays out of its range are re-walked in the reference's order
+            bool tie = false, redo = false;
+            (void)tw_walk<false>(P, o, d, tlo, DINF, h, tie, redo, st);
+            if (__any(tie || redo) && (tie || redo)) {
+                if (tie) c.ties++;
+                ut_closest_call(P, o, d, inv, tlo, time, h, st);
+            }
+            return;
+        }
         (void)ut_walk<false>(P, o, d, inv, tlo, DINF, time, h, st);
     } else {
         intersect_closest<COUNT>(P, o, d, inv, tlo, time, h, st, c);
@@ -59,7 +91,14 @@ __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o
     if (WALK == kWalkTransformed) {
         if (!P.has_tlas) return false;
         Hit hu;
-        return ut_walk<true>(P, o, d, rcp(d), 0.0, tmax, time, hu, st);
+        const V3 inv = rcp(d);
+        if (WIDE && P.wide && P.winst && __all(wide_ok(inv))) {
+            bool tie = false, redo = false;
+            const bool occ = tw_walk<true>(P, o, d, 0.0, tmax, hu, tie, redo, st);
+            if (!redo) return occ;
+            return ut_occluded_call(P, o, d, tmax, time, st);
+        }
+        return ut_walk<true>(P, o, d, inv, 0.0, tmax, time, hu, st);
     }
     return occluded<COUNT>(P, o, d, tmax, time, st, c);
 }
@@ -836,6 +875,7 @@ struct DeviceReplica {
     CTri* ctris = nullptr;
     TriRec* tris = nullptr;
     W4Node* wnodes = nullptr;                 // conservative four-wide walk (wide.h)
+    DWideInst* winst = nullptr;               // ... of transformed scenes: per instance (tw_walk)
     double* lbox = nullptr;
     double* normals = nullptr;
     DInstance* insts = nullptr;
@@ -970,7 +1010,7 @@ static void free_replica(DeviceReplica& r) {
     (void)hipDeviceSynchronize();
     for (void* p : r.retired) (void)hipFree(p);
     r.retired.clear();
-    (void)hipFree(r.wnodes); (void)hipFree(r.lbox);
+    (void)hipFree(r.wnodes); (void)hipFree(r.lbox); (void)hipFree(r.winst);
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.wave_times);
@@ -1053,6 +1093,7 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
         if ((rc = upload(S.wnodes, &r.wnodes, r.bytes)) != RT_OK) return rc;
         if ((rc = upload(S.lbox, &r.lbox, r.bytes)) != RT_OK) return rc;
     }
+    if ((rc = upload(S.winst, &r.winst, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.tlas_leaf, &r.tlas_leaf, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.mats, &r.mats, r.bytes)) != RT_OK) return rc;
@@ -1207,6 +1248,9 @@ static void set_wide(const HostScene& S, const DeviceReplica& r, RenderParams& P
                      int64_t scale_permille) {
     P.wnodes = r.wnodes; P.lbox = r.lbox; P.wide_root = S.wide_root;
     P.wide_copy_bytes = (uint32_t)(S.wide_copy * (int64_t)sizeof(W4Node));
+    P.winst = S.winst.empty() ? nullptr : r.winst;          // transformed scenes (wide.h tw_walk)
+    P.tw_tlas_nodes = (int32_t)S.tw_tlas_nodes;
+    P.tw_wscale = (float)((double)scale_permille * 1e-3);
     const double R = std::max(S.wide_coord, origin_coord) + std::fabs(S.shadow_eps) + std::fabs(S.eps);
     P.wdelta = R * 0x1p-21 * ((double)scale_permille * 1e-3);
     float we = (float)S.eps;
@@ -1710,6 +1754,9 @@ int32_t rt_render_device(rt_scene* s, int32_t slot, int32_t cam, int32_t first, 
     if (step < 1 || first < 0) return fail(RT_ERR_INVALID_ARG, "bad chunk selection");
     int32_t rc = check_renderable(s, cam);
     if (rc != RT_OK) return rc;
+    // the scene's lock: options, scratch growth and its retire list are shared with the submit path
+    // (enqueueing only; rt_render_wait releases the lock while it blocks)
+    std::lock_guard<std::mutex> lock(s->mu);
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's
@@ -1740,6 +1787,9 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
     if (slot < 0 || slot >= (int32_t)s->devs.size()) return fail(RT_ERR_INVALID_ARG, "bad device slot");
     int32_t rc = check_renderable(s, cam);
     if (rc != RT_OK) return rc;
+    // the scene's lock: options, scratch growth and its retire list are shared with the submit path
+    // (enqueueing only; rt_render_wait releases the lock while it blocks)
+    std::lock_guard<std::mutex> lock(s->mu);
     DeviceReplica& r = s->devs[slot];
     HIP_TRY(hipSetDevice(r.device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the default (null) stream, as torch's

@@ -478,8 +478,17 @@ struct WideBuilder {
     HostScene& S;
     std::vector<std::vector<WItem>> groups;
     int depth = 0, max_depth = 0;        // wide levels on the current path / deepest
-    explicit WideBuilder(HostScene& s) : S(s) {}
-    bool terminal(const WItem& x) const { return x.group < 0 && x.ref < 0 && (int64_t)~x.ref < S.tlas_leaf_base; }
+    // transformed scenes (build_wide_tw): a TLAS leaf expands to one marker per instance, carrying
+    // the leaf's box, instead of its instances' BLAS roots; BLASes are built on their own
+    bool tw = false;
+    int64_t marker_base = 0;             // markers are ~(marker_base + instance) (render.hip ut_marker_base)
+    double coord = 0.0;                  // largest |coordinate| of the boxes of the current build
+    explicit WideBuilder(HostScene& s) : S(s), marker_base(s.tlas_leaf_base + (int64_t)s.tlas_leaf.size()) {}
+    bool terminal(const WItem& x) const {
+        if (x.group >= 0 || x.ref >= 0) return false;
+        const int64_t e = ~(int64_t)x.ref;
+        return e < S.tlas_leaf_base || (tw && e >= marker_base);
+    }
     static double area(const WItem& x) {
         const double dx = x.hi[0] - x.lo[0], dy = x.hi[1] - x.lo[1], dz = x.hi[2] - x.lo[2];
         return dx * dy + dy * dz + dz * dx;
@@ -501,8 +510,13 @@ struct WideBuilder {
         for (int64_t e = (int64_t)~x.ref - S.tlas_leaf_base;; ++e) {      // TLAS leaf: instance roots
             const DInstance& I = S.insts[S.tlas_leaf[e].inst];
             WItem w{};
-            for (int k = 0; k < 3; ++k) { w.lo[k] = I.root_lo[k]; w.hi[k] = I.root_hi[k]; }
-            w.ref = I.root_ref;
+            if (tw) {                                    // transformed: a marker with the leaf's box
+                for (int k = 0; k < 3; ++k) { w.lo[k] = x.lo[k]; w.hi[k] = x.hi[k]; }
+                w.ref = (int32_t)~(marker_base + S.tlas_leaf[e].inst);
+            } else {
+                for (int k = 0; k < 3; ++k) { w.lo[k] = I.root_lo[k]; w.hi[k] = I.root_hi[k]; }
+                w.ref = I.root_ref;
+            }
             w.group = -1;
             out.push_back(w);
             if (S.tlas_leaf[e].last) break;
@@ -570,9 +584,11 @@ struct WideBuilder {
         for (size_t i = 0; i < c.size(); ++i) {
             if (terminal(c[i])) {
                 refs[i] = c[i].ref;
-                double* b = &S.lbox[6 * (size_t)~c[i].ref];
+                const int64_t e = ~(int64_t)c[i].ref;
+                double* b = e < S.tlas_leaf_base ? &S.lbox[6 * (size_t)e]                 // leaf run
+                                                 : S.winst[(size_t)(e - marker_base)].tbox;   // marker
                 for (int k = 0; k < 3; ++k) { b[k] = c[i].lo[k]; b[3 + k] = c[i].hi[k]; }
-                S.wide_leaves++;
+                if (e < S.tlas_leaf_base) S.wide_leaves++;
             } else {
                 refs[i] = build(c[i]);                   // preorder: children follow their parent
             }
@@ -584,7 +600,7 @@ struct WideBuilder {
                 if (s < (int)c.size()) {
                     n.pnear[k][s] = down(c[s].lo[k]);
                     n.pfar[k][s] = up(c[s].hi[k]);
-                    S.wide_coord = std::fmax(S.wide_coord, std::fmax(std::fabs(c[s].lo[k]), std::fabs(c[s].hi[k])));
+                    coord = std::fmax(coord, std::fmax(std::fabs(c[s].lo[k]), std::fabs(c[s].hi[k])));
                 } else {
                     n.pnear[k][s] = HUGE_VALF;           // empty slot: never hit (wide.h)
                     n.pfar[k][s] = HUGE_VALF;
@@ -669,6 +685,7 @@ static void build_wide(HostScene& S) {
     if (B.terminal(root)) { S.wnodes.clear(); S.lbox.clear(); S.wide_root = -1; return; }
     S.wnodes.reserve(S.recs.size() / 2 + 16);
     S.wide_root = B.build(root);
+    S.wide_coord = B.coord;
     // a walk holds at most three deferred slots per wide level on its path (plus slack): it must
     // fit the device stack (device.h Stack, kStackCap), else the binary walk
     // (and the walk addresses nodes by 32-bit byte offsets: the array must stay below 4 GB)
@@ -678,6 +695,73 @@ static void build_wide(HostScene& S) {
         S.wnodes.clear(); S.lbox.clear(); S.wide_root = -1;
         return;
     }
+    wide_octant_copies(S);
+}
+
+// Transformed scenes (instances with transforms; static, triangles only): the TLAS collapsed
+// into four-wide nodes whose terminal slots are instance markers carrying their TLAS leaf's box
+// (world space), and every BLAS collapsed on its own (local space; instances of one mesh share
+// it).  The walk (wide.h tw_walk) enters an instance at its marker: the exact FP64 tests of the
+// TLAS leaf box (world ray) and the BLAS root box (local ray) the reference does there
+// (RTContext.swift:632-673, 567-571), then the BLAS's nodes with the instance's local ray.
+static void build_wide_tw(HostScene& S) {
+    S.wnodes.clear(); S.lbox.clear(); S.winst.clear();
+    S.wide_root = -1; S.wide_leaves = 0; S.wide_coord = 0.0; S.tw_tlas_nodes = 0;
+    if (S.has_special || !S.has_tlas || S.max_motion != 0.0 || S.insts.empty()) return;
+    for (const DInstance& I : S.insts)
+        if (I.kind != kPrimTriangles) return;
+    S.lbox.assign(6 * S.tris.size(), 0.0);
+    S.winst.assign(S.insts.size(), DWideInst{});
+    WideBuilder B(S);
+    B.tw = true;
+    WItem root{};
+    for (int k = 0; k < 3; ++k) { root.lo[k] = S.tlas_root_lo[k]; root.hi[k] = S.tlas_root_hi[k]; }
+    root.ref = S.tlas_root_ref;
+    root.group = -1;
+    S.wnodes.reserve(S.recs.size() / 2 + 16);
+    S.wide_root = B.build(root);
+    S.wide_coord = B.coord;
+    S.tw_tlas_nodes = (int64_t)S.wnodes.size();
+    const int tlas_depth = B.max_depth;
+    B.max_depth = 0;
+    std::vector<std::pair<int32_t, std::pair<int32_t, double>>> built;   // BLAS root ref -> (wide root, coord)
+    for (size_t k = 0; k < S.insts.size(); ++k) {
+        const DInstance& I = S.insts[k];
+        int32_t wr = 0;
+        double bc = 0.0;
+        bool found = false;
+        for (const auto& x : built)
+            if (x.first == I.root_ref) { wr = x.second.first; bc = x.second.second; found = true; break; }
+        if (!found) {
+            WItem b{};
+            for (int a = 0; a < 3; ++a) { b.lo[a] = I.root_lo[a]; b.hi[a] = I.root_hi[a]; }
+            b.ref = I.root_ref;
+            b.group = -1;
+            B.coord = 0.0;
+            for (int a = 0; a < 3; ++a) B.coord = std::fmax(B.coord, std::fmax(std::fabs(b.lo[a]), std::fabs(b.hi[a])));
+            if (B.terminal(b)) {                         // a BLAS of one leaf run
+                double* lb = &S.lbox[6 * (size_t)~b.ref];
+                for (int a = 0; a < 3; ++a) { lb[a] = b.lo[a]; lb[3 + a] = b.hi[a]; }
+                S.wide_leaves++;
+                wr = b.ref;
+            } else {
+                wr = B.build(b);
+            }
+            bc = B.coord;
+            built.push_back({I.root_ref, {wr, bc}});
+        }
+        S.winst[k].wroot = wr;
+        S.winst[k].bcoord = bc;
+    }
+    // deepest walk: three deferred slots per wide level on the TLAS path and on the BLAS path,
+    // plus slack; 32-bit byte offsets over the eight copies
+    if (!std::isfinite(S.wide_coord) || 3 * (int64_t)(tlas_depth + B.max_depth) + 4 > kStackCap ||
+        8 * S.wnodes.size() * sizeof(W4Node) >= (size_t(1) << 32)) {
+        S.wnodes.clear(); S.lbox.clear(); S.winst.clear(); S.wide_root = -1; S.tw_tlas_nodes = 0;
+        return;
+    }
+    for (const DWideInst& W : S.winst)
+        if (!std::isfinite(W.bcoord)) { S.wnodes.clear(); S.lbox.clear(); S.winst.clear(); S.wide_root = -1; return; }
     wide_octant_copies(S);
 }
 
@@ -1194,6 +1278,7 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         }
     }
     if (S.identity) build_wide(S);
+    else build_wide_tw(S);
     if (S.recs.size() >= (size_t)INT32_MAX || S.tris.size() >= (size_t)INT32_MAX) { err = "scene too large for int32 refs"; return RT_ERR_UNSUPPORTED; }
     if (maxBlasDepth + 1 > 63 || tlasDepth + 1 > 63) {
         err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550, 623)";

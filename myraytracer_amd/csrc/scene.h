@@ -81,7 +81,11 @@ struct HostScene {
     int64_t wide_leaves = 0;               // reference leaves under the wide tree
     int32_t wide_root = -1;                // -1: no wide tree
     int64_t wide_copy = 0;                 // nodes per octant copy (wnodes holds eight, layout.h W4Node)
-    double wide_coord = 0.0;               // largest |coordinate| of any box (wdelta scale)
+    double wide_coord = 0.0;               // largest |coordinate| of any box (wdelta scale; TLAS boxes
+                                           // for transformed scenes)
+    // transformed scenes (static, triangles only): TLAS nodes first, then every BLAS's nodes
+    std::vector<DWideInst> winst;          // per instance (layout.h DWideInst); empty: identity tree
+    int64_t tw_tlas_nodes = 0;
     // ---- bookkeeping / debug
     int64_t n_meshes = 0, n_tris = 0, n_spheres = 0, n_planes = 0;
     std::vector<uint64_t> inst_bvh_hash;   // per instance: canonical hash of its BLAS

@@ -54,11 +54,11 @@ __device__ __forceinline__ bool wide_ok(const V3& inv) {
     return ax <= 0x1p100 && ax >= 0x1p-100 && ay <= 0x1p100 && ay >= 0x1p-100 && az <= 0x1p100 && az >= 0x1p-100;
 }
 
-__device__ __forceinline__ WRay wide_ray(const RenderParams& P, const V3& o, const V3& inv) {
+__device__ __forceinline__ WRay wide_ray(const RenderParams& P, const V3& o, const V3& inv, double wdelta) {
     WRay r;
     r.ix = (float)inv.x; r.iy = (float)inv.y; r.iz = (float)inv.z;
     const double ox = o.x * inv.x, oy = o.y * inv.y, oz = o.z * inv.z;
-    const double dx = P.wdelta * fabs(inv.x), dy = P.wdelta * fabs(inv.y), dz = P.wdelta * fabs(inv.z);
+    const double dx = wdelta * fabs(inv.x), dy = wdelta * fabs(inv.y), dz = wdelta * fabs(inv.z);
     r.nox = (float)(-ox - dx); r.noy = (float)(-oy - dy); r.noz = (float)(-oz - dz);
     r.fox = (float)(-ox + dx); r.foy = (float)(-oy + dy); r.foz = (float)(-oz + dz);
     const unsigned oct = (inv.x >= 0 ? 0u : 1u) | (inv.y >= 0 ? 0u : 2u) | (inv.z >= 0 ? 0u : 4u);
@@ -138,9 +138,12 @@ __device__ __forceinline__ bool wide_inner(const RenderParams& P, const char* ba
         // Every lane at the same node with the same octant (the top of the tree for a tile's
         // coherent rays): the rows come through the scalar cache into SGPRs once for the wave,
         // instead of 64 copies through the vector-memory data path (TD, ~0.87 busy).
+        // (uoct is a hint: a lane that set it may share the branch with lanes whose ray - another
+        // instance's local ray, tw_walk - has another octant, so the copy is checked too)
         const int r0 = __builtin_amdgcn_readfirstlane(ref);
-        if (__all(ref == r0)) {
-            const unsigned nb = __builtin_amdgcn_readfirstlane(R.obase) + (unsigned)r0 * (unsigned)sizeof(W4Node);
+        const unsigned ob0 = __builtin_amdgcn_readfirstlane(R.obase);
+        if (__all(ref == r0 && R.obase == ob0)) {
+            const unsigned nb = ob0 + (unsigned)r0 * (unsigned)sizeof(W4Node);
             const unsigned long long av = (unsigned long long)(base + (size_t)nb);
             const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
             const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
@@ -208,7 +211,7 @@ __device__ __forceinline__ int tri_candidate(const Tri& T, const V3& o, const V3
 template <bool COUNT, bool SHADOW>
 __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
                                           double tmax, Hit& h, bool& tie, Stack& st, Counts& c) {
-    const WRay R = wide_ray(P, o, inv);
+    const WRay R = wide_ray(P, o, inv, P.wdelta);
     const double eps = P.eps;
     float lim = SHADOW ? wide_limit(P, tmax) : 3.0e38f;
     const int base = st.sp;
@@ -266,6 +269,115 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
             if (ctris ? run(ctris) : run(tris)) { occ = true; break; }
         }
         if (!wide_pop(st, base, lim, ref)) break;
+    }
+    st.reset(base);
+    return occ;
+}
+
+// ---- transformed scenes (static instances with transforms, triangles only; scene.cpp
+// build_wide_tw).  The reference walks the TLAS with the world ray and, at each TLAS leaf, every
+// instance's BLAS with that instance's local ray (RTContext.swift:619-720; the local direction is
+// not renormalised, so t is the same in both spaces).  A triangle is tested iff its TLAS leaf box
+// passes hitAABB with the world ray and its BLAS leaf box with the local ray (box nesting within
+// each tree, wide.h header).  This walk: the TLAS's four-wide nodes in world space (FP32,
+// widened by P.wdelta); a marker slot (its TLAS leaf's box) enters the instance with the exact
+// FP64 tests of the TLAS leaf box (world ray) and of the BLAS root box (local ray, :567-571) -
+// only instances the reference visits are entered - and continues with the BLAS's nodes and the
+// local ray, widened per ray by 2^-21 * max(|BLAS coordinate|, |local origin|) (the bound of the
+// wide.h header for this ray; the FP64 local ray is recomputed per leaf run); candidates are accepted after the exact FP64 test of their leaf
+// box (local).  Stack entries above an instance's marker are its BLAS's, so popping a TLAS entry
+// (node < tw_tlas_nodes, or a marker) brings the world ray back.  Equal-t candidates (tie) and
+// lanes whose local 1/d leaves the FP32 range (redo) are re-walked in the reference's order
+// (device.h ut_walk) by the caller.
+__device__ __forceinline__ bool tw_is_tlas(const RenderParams& P, int ref) {
+    return ref >= 0 ? ref < P.tw_tlas_nodes : ~ref >= P.ut_marker_base;
+}
+template <bool SHADOW>
+__device__ __forceinline__ bool tw_walk(const RenderParams& P, const V3& o, const V3& d, double tlo, double tmax,
+                                        Hit& h, bool& tie, bool& redo, Stack& st) {
+    const double eps = P.eps;
+    WRay R = wide_ray(P, o, rcp(d), P.wdelta);
+    float lim = SHADOW ? wide_limit(P, tmax) : 3.0e38f;
+    const int base = st.sp;
+    int ref = P.wide_root;
+    int inst = -1;
+    bool occ = false;
+    const char* wbase = reinterpret_cast<const char*>(P.wnodes);
+    const auto* ctris = P.ctris;
+    const auto* tris = P.tris;
+    for (;;) {
+        if (ref >= 0) {
+            if (wide_inner(P, wbase, ref, R, lim, st)) continue;
+        } else if (~ref >= P.ut_marker_base) {
+            // enter instance k: the reference's TLAS leaf test (world) and BLAS root test (local)
+            const int k = ~ref - P.ut_marker_base;
+            const DWideInst& WI = P.winst[k];
+            const double limd = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+            const V3 inv = rcp(d);
+            double dt;
+            if (slab_hit<true>(WI.tbox[0], WI.tbox[1], WI.tbox[2], WI.tbox[3], WI.tbox[4], WI.tbox[5], o, inv, eps, dt) &&
+                !(dt > limd)) {
+                const DInstance& I = P.insts[k];
+                const V3 ol2 = m4_point(I.w2l, o, 1.0), dl2 = m4_point(I.w2l, d, 0.0);
+                const V3 il = rcp(dl2);
+                if (!wide_ok(il)) { redo = true; break; }
+                double dr;
+                if (slab_hit<true>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1], I.root_hi[2],
+                                   ol2, il, eps, dr) && !(dr > limd)) {
+                    inst = k;
+                    const double oc = fmax(fmax(fabs(ol2.x), fabs(ol2.y)), fabs(ol2.z));
+                    R = wide_ray(P, ol2, il, 0x1p-21 * (double)P.tw_wscale * fmax(WI.bcoord, oc));
+                    ref = WI.wroot;
+                    continue;
+                }
+            }
+        } else {
+            const int t0 = ~ref;                          // a BLAS leaf run of instance `inst`
+            int box = 0;                                   // leaf box: 0 unchecked, 1 passes, 2 fails
+            // the local ray, recomputed (the same arithmetic as at the marker) rather than kept
+            // live beside the world ray across the walk
+            const DInstance& I = P.insts[inst];
+            const V3 ol = m4_point(I.w2l, o, 1.0), dl = m4_point(I.w2l, d, 0.0);
+            auto leaf_ok = [&]() {
+                const double* b = P.lbox + 6 * (size_t)t0;
+                double tm;
+                return slab_hit<true>(b[0], b[1], b[2], b[3], b[4], b[5], ol, rcp(dl), eps, tm);
+            };
+            auto run = [&](const auto* tris) {
+                for (int t = t0;; ++t) {
+                    const auto T = tris[t];
+                    if (SHADOW) {
+                        if (tri_shadow(T, ol, dl, 0.0, tmax, eps, P.fast_rcp)) {
+                            if (box == 0) box = leaf_ok() ? 1 : 2;
+                            if (box == 1) return true;
+                        }
+                    } else {
+                        double tt, uu, vv;
+                        const int r = tri_candidate(T, ol, dl, tlo, eps, h.t, tt, uu, vv, P.fast_rcp);
+                        if (r != 0) {
+                            if (box == 0) box = leaf_ok() ? 1 : 2;
+                            if (box == 1) {
+                                if (r == 1) {
+                                    h.t = tt; h.u = uu; h.v = vv; h.tri = t; h.inst = inst;
+                                    tie = false;
+                                    lim = wide_limit(P, tt);
+                                } else {
+                                    tie = true;
+                                }
+                            }
+                        }
+                    }
+                    if (T.last) break;
+                }
+                return false;
+            };
+            if (ctris ? run(ctris) : run(tris)) { occ = true; break; }
+        }
+        if (!wide_pop(st, base, lim, ref)) break;
+        if (inst >= 0 && tw_is_tlas(P, ref)) {            // back to the world ray
+            inst = -1;
+            R = wide_ray(P, o, rcp(d), P.wdelta);
+        }
     }
     st.reset(base);
     return occ;

@@ -205,7 +205,7 @@ def test_bench_strong_split_two_ranks_gathers_the_same_frame():
     assert two["rays"]["per_step"] == one["rays"]["per_step"]
 
 
-@pytest.mark.timeout(480)
+@pytest.mark.timeout(600)
 def test_bench_strong_split_eight_ranks_on_one_gpu():
     """The C4 process path at N = 8 (Object+Extension.swift:75-82): `bench.py --gpus 8` with
     every rank pinned to this GPU (MYRT_BENCH_DEVICE=0, 32 / 8 = 4 hardware queues per rank),
@@ -230,6 +230,19 @@ def test_bench_strong_split_eight_ranks_on_one_gpu():
     assert staged["gather"]["mode"] == "staged" and staged["gather"]["rows_complete"]
     assert staged["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
     assert staged["per_rank"]["gather"] == "staged" and len(staged["per_rank"]["device_ms_per_frame"]) == 8
+    # NUMA: every rank's GPU node, CPU affinity and the node of its frame pages;
+    # the opt-in first-touch placement (each rank binds to its GPU's node and touches its own rows
+    # before registration) gathers the same image
+    for line in (eight, staged):
+        assert len(line["per_rank"]["numa"]) == 8
+        for r in line["per_rank"]["numa"]:
+            assert "node" in r["gpu"] and r["affinity"] and "frame_pages_by_node" in r
+    assert sum(sum(r["frame_pages_by_node"].values()) for r in eight["per_rank"]["numa"]) > 0
+    placed = _bench(["--gpus", "8", "--numa", "first-touch"] + common, {"MYRT_BENCH_DEVICE": "0"})
+    assert placed["gather"]["rows_complete"]
+    assert placed["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
+    assert all(r["placement"] == "first-touch" for r in placed["per_rank"]["numa"])
+    assert one["numa"]["gpu"] is not None and "scratch_bytes_after_warmup" in one["scene"]
 
 
 @pytest.mark.timeout(400)

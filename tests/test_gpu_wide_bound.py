@@ -261,3 +261,67 @@ def test_the_sets_reach_the_bound():
     # and 226 / 6000 touching occlusion results differ without the widening
     assert bad0.any(), "near-vertex rays: no mismatch without widening, the set does not reach the bound"
     assert badt0.any() and occ0.any(), "touching rays: no mismatch without widening"
+
+
+def _rot(rng):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def _far_instances():
+    """C2's mesh far from the origin in its own space (1e6) under three rotated / scaled /
+    translated instances placed far from the world origin (the four-wide transformed walk,
+    wide.h tw_walk: world-space TLAS, local-space BLAS widened per ray)."""
+    sc, scale, off = _far_c2("1e6")
+    base = sc.objects[0]
+    rng = np.random.RandomState(77)
+    mats = []
+    for k in range(3):
+        M4 = np.eye(4)
+        M4[:3, :3] = _rot(rng) * (0.5 + 0.4 * k)
+        M4[:3, 3] = np.array([-3.0e5, 7.0e5, 2.0e5]) + rng.uniform(-1, 1, size=3) * 8.0e4 - M4[:3, :3] @ off
+        mats.append(M4)
+    base.transform = tuple(mats[0].T.reshape(-1))
+    sc.objects = [base] + [M.MeshInstance(id=50 + k, base_mesh_id=base.id, material="1",
+                                          transform=tuple(mats[k].T.reshape(-1))) for k in (1, 2)]
+    centre = np.array([-3.0e5, 7.0e5, 2.0e5])
+    sc.cameras[0].position = tuple(centre + np.array([0.0, 2.0e4, 9.0e4]))
+    sc.cameras[0].gaze_point = tuple(centre)
+    sc.point_lights[0].position = tuple(centre + np.array([4.0e4, 9.0e4, 6.0e4]))
+    return sc, mats, centre
+
+
+def test_transformed_instances_far_away_and_teeth():
+    """Near-vertex rays at instances of a far mesh (world and local coordinates ~1e6): bit-exact
+    closest hits and occlusion through the four-wide transformed walk, and the frame; without the
+    widening (wide_delta_scale = 0, world and local) the same rays differ from the oracle."""
+    sc, mats, centre = _far_instances()
+    mesh = sc.objects[0]
+    P, F = np.asarray(mesh.positions), np.asarray(mesh.indices)
+    rng = np.random.RandomState(91)
+    Os, Ds = [], []
+    for M4 in mats:
+        Pw = P @ M4[:3, :3].T + M4[:3, 3]
+        O, D = _near_vertex_rays(Pw, F, 5000, rng, 4.0e4)
+        Os.append(O); Ds.append(D)
+    O, D = np.concatenate(Os), np.concatenate(Ds)
+    orc = oracle.OracleScene(sc)
+    bad, hit = _closest_mismatch(sc, O, D, orc=orc)
+    assert not bad.any(), f"{int(bad.sum())} of {len(O)} closest hits differ"
+    assert hit.mean() > 0.3
+    t, *_ = orc.trace_rays(O, D)
+    tmax = np.where(np.isfinite(t), t * (1 + rng.choice([-1e-9, 1e-9], size=len(t))), 1e7)
+    bado, occ = _occluded_mismatch(sc, O, D, tmax, orc=orc)
+    assert not bado.any()
+    eng = _engine(sc)
+    rgb, rgba, st = eng.render_rows(0, 0, 1, True)
+    eng.close()
+    ref, ref8, _ = orc.render(0, 0, 1, threads=0, rgba=True)
+    assert float(np.abs(rgb - ref).max()) <= TOL and np.array_equal(rgba, ref8)
+    bad0, _ = _closest_mismatch(sc, O, D, permille=0, orc=orc)
+    print(f"transformed, no widening: {int(bad0.sum())} / {len(O)} closest hits differ")
+    assert bad0.any(), "no mismatch without widening: the set does not reach the bound"

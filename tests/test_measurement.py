@@ -211,3 +211,22 @@ def test_isa_loops_census():
     assert rows["BB0_1"]["depth"] == 1 and rows["BB0_1"]["readlane"] == 1 and rows["BB0_1"]["writelane"] == 1
     assert rows["BB0_1"]["s_load"] == 1 and rows["BB0_1"]["valu"] == 3
     assert rows["BB0_2"]["depth"] == 2 and rows["BB0_2"]["scratch_ld"] == 1 and rows["BB0_2"]["valu"] == 1
+
+
+def test_numa_helpers():
+    """bench.py's NUMA fields: cpulist parsing / printing, the node map from
+    sysfs, and the per-page node census of a buffer (move_pages with no target nodes)."""
+    import numpy as np
+    assert bench._cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert bench._ranges({0, 1, 2, 3, 8, 10, 11}) == "0-3,8,10-11"
+    nodes = bench.numa_nodes()
+    assert all(isinstance(k, int) and v for k, v in nodes.items())
+    a = np.zeros(1 << 20, np.uint8)
+    a[:] = 1                                          # every page present
+    got = bench.pages_by_node(a.ctypes.data, a.nbytes)
+    if got is not None:                               # move_pages may be refused in a sandbox
+        pg = os.sysconf("SC_PAGE_SIZE")
+        assert sum(got.values()) >= a.nbytes // pg
+        if nodes:
+            assert set(int(k) for k in got) <= set(nodes)
+    assert bench.pages_by_node(a.ctypes.data, 0) == {}

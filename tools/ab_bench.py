@@ -2,6 +2,7 @@
 interleaved over rounds, one summary line per run (value, ms/frame, one-launch kernel ms).
 
 usage: tools/ab_bench.py PREFIX CONFIG STEPS ROUNDS NAME[:ENV=VAL[,ENV=VAL...]] ...
+  (a key opt.NAME passes --option NAME=VAL to bench.py instead of setting the environment)
   e.g. tools/ab_bench.py r05b c3 1000 2 base:MYRT_LIB=build_variants/libmyrt_base.so main
 Each run: python bench.py --config CONFIG --steps STEPS --no-cpu-baseline --no-side-paths, its
 JSON line written to gpurun_out/PREFIX_bench_CONFIG_NAME[_k].json and summarised on stdout.
@@ -26,10 +27,14 @@ def main():
     for r in range(rounds):
         for name, env in variants:
             e = dict(os.environ)
+            opts = []
             for k, v in env.items():
-                e[k] = os.path.join(ROOT, v) if k == "MYRT_LIB" else v
+                if k.startswith("opt."):                 # opt.NAME=VALUE: bench --option NAME=VALUE
+                    opts += ["--option", f"{k[4:]}={v}"]
+                else:
+                    e[k] = os.path.join(ROOT, v) if k == "MYRT_LIB" else v
             cmd = [sys.executable, "bench.py", "--config", cfg, "--steps", str(steps), "--no-cpu-baseline",
-                   "--no-side-paths"]
+                   "--no-side-paths"] + opts
             p = subprocess.run(["timeout", "-k", "10", "300"] + cmd, cwd=ROOT, env=e, capture_output=True, text=True)
             if p.returncode != 0:
                 print(f"{name}: rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
