@@ -83,7 +83,7 @@ def parse():
                         "one shared page-locked framebuffer; staged = rows delivered by each GPU's DMA engine "
                         "into a private page-locked frame, then copied by the rank's host thread into the "
                         "shared frame (no concurrent PCIe stores from 8 GPUs into one segment)")
-    p.add_argument("--numa", default="none", choices=["none", "first-touch"],
+    p.add_argument("--numa-placement", default="none", choices=["none", "first-touch"],
                    help="N > 1 strong, shared gather: first-touch = each rank binds its CPU affinity to its GPU's "
                         "NUMA node (when the process may run there) and touches its own rows of every shared "
                         "frame before any rank registers it, so those pages live on its GPU's socket; none = "
@@ -269,8 +269,8 @@ def main():
     # NUMA: this rank's GPU node, CPU affinity, and (opt-in) the affinity bound to the GPU's node
     nodes = numa_nodes()
     gnode = gpu_numa_node(local)
-    numa = {"gpu": gnode, "placement": args.numa, "affinity_before": _ranges(os.sched_getaffinity(0))}
-    if args.numa == "first-touch" and gnode.get("node") is not None and gnode["node"] in nodes:
+    numa = {"gpu": gnode, "placement": args.numa_placement, "affinity_before": _ranges(os.sched_getaffinity(0))}
+    if args.numa_placement == "first-touch" and gnode.get("node") is not None and gnode["node"] in nodes:
         want = set(nodes[gnode["node"]]) & os.sched_getaffinity(0)
         if want:
             os.sched_setaffinity(0, want)
@@ -337,7 +337,7 @@ def main():
         for q in range(Q):
             sf = SharedFrame(W * H * 4, rank, world, dist, f"{args.config}{q}")
             shared.append(sf)
-        if args.numa == "first-touch" and not staged:
+        if args.numa_placement == "first-touch" and not staged:
             # every rank first-touches its own rows (8-row chunks c = rank mod world) while bound to
             # its GPU's node; registration (which faults every page it touches first) waits for all
             for sf in shared:
@@ -552,7 +552,7 @@ def main():
                      "rewalked_what": "closest-hit rays of rank 0's share that the four-wide walk handed to the "
                                       "reference-order walk (two candidates at the final t, wide.h)"},
             "per_rank": per_rank,
-            "numa": numa if world == 1 else {"placement": args.numa, "per_rank": "per_rank.numa"},
+            "numa": numa if world == 1 else {"placement": args.numa_placement, "per_rank": "per_rank.numa"},
             "scene": {"device_bytes": int(info.device_bytes), "scratch_bytes_after_warmup": scratch_after_warmup,
                       "build_ms": round(float(info.build_ms), 1), "upload_ms": round(float(info.upload_ms), 1)},
             "timing": {"in_flight": Q, "submit_to_done_ms": round(statistics.mean(calls), 4),

@@ -70,7 +70,7 @@ __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o,
             // the four-wide walk of transformed scenes (wide.h tw_walk); equal-t candidates and
             // local rays out of its range are re-walked in the reference's order
             bool tie = false, redo = false;
-            (void)tw_walk<false>(P, o, d, tlo, DINF, h, tie, redo, st);
+            (void)tw_walk<false>(P, TwWorld{o, d}, tlo, DINF, h, tie, redo, st);
             if (__any(tie || redo) && (tie || redo)) {
                 if (tie) c.ties++;
                 ut_closest_call(P, o, d, inv, tlo, time, h, st);
@@ -83,8 +83,30 @@ __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o,
     }
 }
 
+// The megakernel's closest hit of a transformed scene with the world ray parked (wide.h
+// TwParked): the caller stores it before and reads it back after, so it is not live across the
+// walk (MYRT_TW_PARK).
+#ifndef MYRT_TW_PARK
+#define MYRT_TW_PARK 1
+#endif
+template <bool COUNT>
+__device__ __forceinline__ void walk_closest_tw_parked(const RenderParams& P, const TwParked& pk, double tlo,
+                                                       double time, Hit& h, Stack& st, Counts& c) {
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    if (P.wide && P.winst && __all(wide_ok(rcp(pk.d())))) {
+        bool tie = false, redo = false;
+        (void)tw_walk<false>(P, pk, tlo, DINF, h, tie, redo, st);
+        if (__any(tie || redo) && (tie || redo)) {
+            if (tie) c.ties++;
+            ut_closest_call(P, pk.o(), pk.d(), rcp(pk.d()), tlo, time, h, st);
+        }
+        return;
+    }
+    (void)ut_walk<false>(P, pk.o(), pk.d(), rcp(pk.d()), tlo, DINF, time, h, st);
+}
+
 // Any hit of one shadow ray (tMin 0, tMax) by the scene's walk.
-template <bool COUNT, int WALK, bool WIDE = true>
+template <bool COUNT, int WALK, bool WIDE = true, bool PARK = (MYRT_TW_PARK != 0)>
 __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time,
                                               Stack& st, Counts& c) {
     if (WALK == kWalkIdentity) return uni_occluded<COUNT, WIDE>(P, o, d, tmax, st, c);
@@ -94,7 +116,14 @@ __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o
         const V3 inv = rcp(d);
         if (WIDE && P.wide && P.winst && __all(wide_ok(inv))) {
             bool tie = false, redo = false;
-            const bool occ = tw_walk<true>(P, o, d, 0.0, tmax, hu, tie, redo, st);
+            bool occ;
+            if (PARK) {
+                TwParked pk;
+                pk.store(o, d);
+                occ = tw_walk<true>(P, pk, 0.0, tmax, hu, tie, redo, st);
+            } else {
+                occ = tw_walk<true>(P, TwWorld{o, d}, 0.0, tmax, hu, tie, redo, st);
+            }
             if (!redo) return occ;
             return ut_occluded_call(P, o, d, tmax, time, st);
         }
@@ -261,7 +290,15 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         const V3 inv = rcp(d);
         Hit h;
         park();
-        walk_closest<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE>(P, o, d, inv, tlo, time, h, st, c);
+        if (WALK == kWalkTransformed && MYRT_TW_PARK && (!BOUNCE || MYRT_BOUNCE_WIDE)) {
+            TwParked pk;                                  // the world ray waits in private memory
+            pk.store(o, d);
+            walk_closest_tw_parked<COUNT>(P, pk, tlo, time, h, st, c);
+            o = pk.o();
+            d = pk.d();
+        } else {
+            walk_closest<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE>(P, o, d, inv, tlo, time, h, st, c);
+        }
         unpark();
         if (h.inst < 0) { L = ld3(P.background); break; }
         V3 p, Ngeo;
@@ -770,7 +807,7 @@ __global__ __launch_bounds__(256) void k_trace_rays(RenderParams P, RayBatch B) 
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     if (P.has_tlas) {
         if (B.uni == 1) uni_closest<false>(P, o, d, rcp(d), B.tlim[i], h, st, c);
-        else if (B.uni == 2) (void)ut_walk<false>(P, o, d, rcp(d), B.tlim[i], DINF, time, h, st);
+        else if (B.uni == 2) walk_closest<false, kWalkTransformed>(P, o, d, rcp(d), B.tlim[i], time, h, st, c);
         else intersect_closest<false>(P, o, d, rcp(d), B.tlim[i], time, h, st, c);
     }
     V3 p = v3(0, 0, 0), n = v3(0, 0, 0);
@@ -787,9 +824,8 @@ __global__ __launch_bounds__(256) void k_occluded_rays(RenderParams P, RayBatch 
     MYRT_STACK(st, lds_stack);
     Counts c{};
     const V3 o = v3(B.o[3 * i], B.o[3 * i + 1], B.o[3 * i + 2]), d = v3(B.d[3 * i], B.d[3 * i + 1], B.d[3 * i + 2]);
-    Hit hu;
     const bool hit = B.uni == 1 ? uni_occluded<false>(P, o, d, B.tlim[i], st, c)
-                     : B.uni == 2 ? (P.has_tlas && ut_walk<true>(P, o, d, rcp(d), 0.0, B.tlim[i], B.time[i], hu, st))
+                     : B.uni == 2 ? walk_occluded<false, kWalkTransformed, true, false>(P, o, d, B.tlim[i], B.time[i], st, c)
                            : occluded<false>(P, o, d, B.tlim[i], B.time[i], st, c);
     B.out_occ[i] = hit ? 1 : 0;
 }

@@ -284,7 +284,7 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
 // FP64 tests of the TLAS leaf box (world ray) and of the BLAS root box (local ray, :567-571) -
 // only instances the reference visits are entered - and continues with the BLAS's nodes and the
 // local ray, widened per ray by 2^-21 * max(|BLAS coordinate|, |local origin|) (the bound of the
-// wide.h header for this ray; the FP64 local ray is recomputed per leaf run); candidates are accepted after the exact FP64 test of their leaf
+// wide.h header for this ray); candidates are accepted after the exact FP64 test of their leaf
 // box (local).  Stack entries above an instance's marker are its BLAS's, so popping a TLAS entry
 // (node < tw_tlas_nodes, or a marker) brings the world ray back.  Equal-t candidates (tie) and
 // lanes whose local 1/d leaves the FP32 range (redo) are re-walked in the reference's order
@@ -292,15 +292,43 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, co
 __device__ __forceinline__ bool tw_is_tlas(const RenderParams& P, int ref) {
     return ref >= 0 ? ref < P.tw_tlas_nodes : ~ref >= P.ut_marker_base;
 }
-template <bool SHADOW>
-__device__ __forceinline__ bool tw_walk(const RenderParams& P, const V3& o, const V3& d, double tlo, double tmax,
+// The world ray of a transformed walk: kept by the caller (TwWorld) or parked in this lane's
+// private memory (TwParked: read back only where the walk needs it - its start, an instance's
+// marker, the return to the TLAS - so it is not live, spilled, across the BLAS walks; the empty
+// asm with the array's address keeps the compiler from forwarding the stored values.  1/d is
+// recomputed there: parking it too, or a volatile park, measured slower, profiles/r05h_ab_c3i.txt).
+struct TwWorld {
+    const V3& o_;
+    const V3& d_;
+    __device__ __forceinline__ V3 o() const { return o_; }
+    __device__ __forceinline__ V3 d() const { return d_; }
+    static constexpr bool kParked = false;
+};
+struct TwParked {
+    double v[6];                                          // o, d
+    __device__ __forceinline__ void store(const V3& o, const V3& d) {
+        v[0] = o.x; v[1] = o.y; v[2] = o.z; v[3] = d.x; v[4] = d.y; v[5] = d.z;
+        asm volatile("" :: "v"(&v[0]) : "memory");
+    }
+    __device__ __forceinline__ V3 o() const { asm volatile("" :: "v"(&v[0]) : "memory"); return v3(v[0], v[1], v[2]); }
+    __device__ __forceinline__ V3 d() const { asm volatile("" :: "v"(&v[0]) : "memory"); return v3(v[3], v[4], v[5]); }
+    static constexpr bool kParked = true;
+};
+
+template <bool SHADOW, class World>
+__device__ __forceinline__ bool tw_walk(const RenderParams& P, const World& W, double tlo, double tmax,
                                         Hit& h, bool& tie, bool& redo, Stack& st) {
     const double eps = P.eps;
-    WRay R = wide_ray(P, o, rcp(d), P.wdelta);
+    WRay R;
+    {
+        const V3 o = W.o(), d = W.d();
+        R = wide_ray(P, o, rcp(d), P.wdelta);
+    }
     float lim = SHADOW ? wide_limit(P, tmax) : 3.0e38f;
     const int base = st.sp;
     int ref = P.wide_root;
     int inst = -1;
+    V3 ol = v3(0, 0, 0), dl = v3(0, 0, 0);             // the local ray (kept when the world ray is parked)
     bool occ = false;
     const char* wbase = reinterpret_cast<const char*>(P.wnodes);
     const auto* ctris = P.ctris;
@@ -313,6 +341,7 @@ __device__ __forceinline__ bool tw_walk(const RenderParams& P, const V3& o, cons
             const int k = ~ref - P.ut_marker_base;
             const DWideInst& WI = P.winst[k];
             const double limd = (SHADOW ? tmax : h.t) * P.prune_rel + P.prune_abs;
+            const V3 o = W.o(), d = W.d();
             const V3 inv = rcp(d);
             double dt;
             if (slab_hit<true>(WI.tbox[0], WI.tbox[1], WI.tbox[2], WI.tbox[3], WI.tbox[4], WI.tbox[5], o, inv, eps, dt) &&
@@ -325,6 +354,7 @@ __device__ __forceinline__ bool tw_walk(const RenderParams& P, const V3& o, cons
                 if (slab_hit<true>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1], I.root_hi[2],
                                    ol2, il, eps, dr) && !(dr > limd)) {
                     inst = k;
+                    if (World::kParked) { ol = ol2; dl = dl2; }
                     const double oc = fmax(fmax(fabs(ol2.x), fabs(ol2.y)), fabs(ol2.z));
                     R = wide_ray(P, ol2, il, 0x1p-21 * (double)P.tw_wscale * fmax(WI.bcoord, oc));
                     ref = WI.wroot;
@@ -334,10 +364,13 @@ __device__ __forceinline__ bool tw_walk(const RenderParams& P, const V3& o, cons
         } else {
             const int t0 = ~ref;                          // a BLAS leaf run of instance `inst`
             int box = 0;                                   // leaf box: 0 unchecked, 1 passes, 2 fails
-            // the local ray, recomputed (the same arithmetic as at the marker) rather than kept
-            // live beside the world ray across the walk
-            const DInstance& I = P.insts[inst];
-            const V3 ol = m4_point(I.w2l, o, 1.0), dl = m4_point(I.w2l, d, 0.0);
+            // the local ray: kept (parked world ray), or recomputed with the marker's arithmetic
+            // rather than kept live beside the world ray across the walk
+            if (!World::kParked) {
+                const DInstance& I = P.insts[inst];
+                ol = m4_point(I.w2l, W.o(), 1.0);
+                dl = m4_point(I.w2l, W.d(), 0.0);
+            }
             auto leaf_ok = [&]() {
                 const double* b = P.lbox + 6 * (size_t)t0;
                 double tm;
@@ -376,6 +409,7 @@ __device__ __forceinline__ bool tw_walk(const RenderParams& P, const V3& o, cons
         if (!wide_pop(st, base, lim, ref)) break;
         if (inst >= 0 && tw_is_tlas(P, ref)) {            // back to the world ray
             inst = -1;
+            const V3 o = W.o(), d = W.d();
             R = wide_ray(P, o, rcp(d), P.wdelta);
         }
     }

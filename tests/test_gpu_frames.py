@@ -238,7 +238,7 @@ def test_bench_strong_split_eight_ranks_on_one_gpu():
         for r in line["per_rank"]["numa"]:
             assert "node" in r["gpu"] and r["affinity"] and "frame_pages_by_node" in r
     assert sum(sum(r["frame_pages_by_node"].values()) for r in eight["per_rank"]["numa"]) > 0
-    placed = _bench(["--gpus", "8", "--numa", "first-touch"] + common, {"MYRT_BENCH_DEVICE": "0"})
+    placed = _bench(["--gpus", "8", "--numa-placement", "first-touch"] + common, {"MYRT_BENCH_DEVICE": "0"})
     assert placed["gather"]["rows_complete"]
     assert placed["gather"]["rgba8_sha256"] == one["gather"]["rgba8_sha256"]
     assert all(r["placement"] == "first-touch" for r in placed["per_rank"]["numa"])
