@@ -133,11 +133,13 @@ __device__ __forceinline__ int xcd_tile(int b, int nb, int G) {
 // An entry packs {ref (low 32), high 32 bits of the entry distance (high 32)}: dropping
 // the low mantissa word truncates toward zero, i.e. rounds a positive distance DOWN, so
 // pop-time culling stays conservative (negative distances are never culled).
-// LDS entries per lane: 16 since the four-wide walk (up to three pushes per node; C3 +1.2 %,
-// C5 +1.6 % over 8, profiles/r04g_*).  16 entries + the 4 pixel slots = 10 KB per wave: the
-// 16 waves of a CU at 4 waves/SIMD fill its 160 KB exactly.
+// LDS entries per lane: 16 in round 4 (the sorted four-wide walk pushed up to three entries per
+// node; C3 +1.2 %, C5 +1.6 % over 8, profiles/r04g_*); 10 since round 5 - with the octant-ordered
+// walk C3 is the same at 10, 12 and 16 (8,605 / 8,604 / 8,611 Mrays/s, profiles/r05l_ab_c3.txt,
+// r05m_ab_c3.txt) - so the megakernel's 10 stack entries + 4 pixel slots + 6 world-ray park slots
+// (render.hip TwParkedLds) are 10 KB per wave: the 16 waves of a CU at 4 waves/SIMD fill its 160 KB.
 #ifndef MYRT_KLDS
-#define MYRT_KLDS 16
+#define MYRT_KLDS 10
 #endif
 constexpr int kLds = MYRT_KLDS;
 constexpr int kSpill = kStackCap - kLds;   // the host refuses deeper scenes (scene.cpp, RT_ERR_STACK)

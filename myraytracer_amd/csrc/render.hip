@@ -89,8 +89,8 @@ __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o,
 #ifndef MYRT_TW_PARK
 #define MYRT_TW_PARK 1
 #endif
-template <bool COUNT>
-__device__ __forceinline__ void walk_closest_tw_parked(const RenderParams& P, const TwParked& pk, double tlo,
+template <bool COUNT, class Park>
+__device__ __forceinline__ void walk_closest_tw_parked(const RenderParams& P, const Park& pk, double tlo,
                                                        double time, Hit& h, Stack& st, Counts& c) {
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     if (P.wide && P.winst && __all(wide_ok(rcp(pk.d())))) {
@@ -239,6 +239,11 @@ __device__ __forceinline__ void store_pixel(const RenderParams& P, int i, int j,
 }
 
 constexpr int kPixSlots = 4;   // per lane: pixel sum x/y/z and the parked PCG32 state, after the stacks
+// then, with MYRT_TW_LDS, kParkSlots doubles per lane where a transformed walk parks its world ray
+#ifndef MYRT_TW_LDS
+#define MYRT_TW_LDS 1     // C3i 4,535 -> 4,956 Mrays/s against the private-memory park (profiles/r05m_ab_c3i.txt)
+#endif
+constexpr int kParkSlots = MYRT_TW_LDS ? 6 : 0;
 constexpr int kTileW = 8;      // 8x8 pixel tiles (16x4 / 32x2 measured slower: DESIGN.md §4)
 typedef __attribute__((address_space(3))) double lds_f64;
 // This lane's index in its (one-wave) block, computed afresh: the empty asm keeps the compiler from
@@ -254,6 +259,24 @@ __device__ __forceinline__ lds_f64* pix_slot(int k) {
     extern __shared__ unsigned long long lds_stack[];
     return (lds_f64*)(lds_u64*)(lds_stack + 64 * kLds) + k * 64 + pix_lane();
 }
+
+// The megakernel's world-ray park in LDS (MYRT_TW_LDS): the slots after the pixel slots, read
+// back where the transformed walk needs the world ray (wide.h tw_walk, TwParked's interface).
+struct TwParkedLds {
+    __device__ __forceinline__ static lds_f64* at(int k) { return pix_slot(kPixSlots + k); }
+    __device__ __forceinline__ void store(const V3& o, const V3& d) const {
+        *at(0) = o.x; *at(1) = o.y; *at(2) = o.z; *at(3) = d.x; *at(4) = d.y; *at(5) = d.z;
+        asm volatile("" ::: "memory");
+    }
+    __device__ __forceinline__ V3 o() const { asm volatile("" ::: "memory"); return v3(*at(0), *at(1), *at(2)); }
+    __device__ __forceinline__ V3 d() const { asm volatile("" ::: "memory"); return v3(*at(3), *at(4), *at(5)); }
+    static constexpr bool kParked = true;
+};
+#if MYRT_TW_LDS
+typedef TwParkedLds TwPark;
+#else
+typedef TwParked TwPark;
+#endif
 
 // trace() (Object+Extension.swift:96-283) for diffuse/mirror/conductor materials and
 // point lights.  The recursion Lo + M*trace(depth+1) is run forward and combined
@@ -291,7 +314,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         Hit h;
         park();
         if (WALK == kWalkTransformed && MYRT_TW_PARK && (!BOUNCE || MYRT_BOUNCE_WIDE)) {
-            TwParked pk;                                  // the world ray waits in private memory
+            TwPark pk;                                    // the world ray waits in private memory / LDS
             pk.store(o, d);
             walk_closest_tw_parked<COUNT>(P, pk, tlo, time, h, st, c);
             o = pk.o();
@@ -1627,7 +1650,8 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     const int bt = kRenderBlock;
     dim3 grid = render_grid(P, bt, dev::kTileW);
     dim3 block((unsigned)bt, 1, 1);
-    const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long) + (size_t)dev::kPixSlots * bt * sizeof(double);
+    const size_t lds = (size_t)dev::kLds * bt * sizeof(unsigned long long) +
+                       (size_t)(dev::kPixSlots + dev::kParkSlots) * bt * sizeof(double);
     const bool bounce = scene_has_bounce(s->host) && P.max_depth > 0;
     // The walk: identity scenes walk TLAS + BLAS as one tree; other scenes the unified transformed
     // walk (per-instance ray switches), or the nested general walk when the stack bound does not
