@@ -106,7 +106,7 @@ __device__ __forceinline__ void walk_closest_tw_parked(const RenderParams& P, co
 }
 
 // Any hit of one shadow ray (tMin 0, tMax) by the scene's walk.
-template <bool COUNT, int WALK, bool WIDE = true, bool PARK = (MYRT_TW_PARK != 0)>
+template <bool COUNT, int WALK, bool WIDE = true, bool PARK = (MYRT_TW_PARK != 0), class WPark = TwParked>
 __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time,
                                               Stack& st, Counts& c) {
     if (WALK == kWalkIdentity) return uni_occluded<COUNT, WIDE>(P, o, d, tmax, st, c);
@@ -118,7 +118,7 @@ __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o
             bool tie = false, redo = false;
             bool occ;
             if (PARK) {
-                TwParked pk;
+                WPark pk;                                 // private memory, or the megakernel's LDS slots
                 pk.store(o, d);
                 occ = tw_walk<true>(P, pk, 0.0, tmax, hu, tie, redo, st);
             } else {
@@ -136,7 +136,7 @@ __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o
 // terms to Lo.  With !(N.L > 0) the reference discards the occlusion result, so that walk is
 // skipped; the ray is still counted as cast.
 // park/unpark: the caller's PCG32 state moves to LDS around each walk (trace_path BOUNCE).
-template <bool COUNT, int WALK, bool WIDE, class Park, class Unpark>
+template <bool COUNT, int WALK, bool WIDE, class WPark = TwParked, class Park, class Unpark>
 __device__ __forceinline__ void point_lights(const RenderParams& P, const DMaterial& M, const V3& N, const V3& p,
                                              const V3& d, double time, Stack& st, Counts& c, V3& Lo, Park park,
                                              Unpark unpark) {
@@ -167,7 +167,7 @@ __device__ __forceinline__ void point_lights(const RenderParams& P, const DMater
         if (NdotL > 0 || MYRT_REF(P)) {
             c.shadow_traced++;
             park();
-            const bool blocked = walk_occluded<COUNT, WALK, WIDE>(P, so, wi, dist, time, st, c);
+            const bool blocked = walk_occluded<COUNT, WALK, WIDE, (MYRT_TW_PARK != 0), WPark>(P, so, wi, dist, time, st, c);
             unpark();
             if (!blocked && NdotL > 0) Lo = Lo + contrib;
         }
@@ -354,7 +354,7 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
             }
         }
         if (computeDirect)
-            point_lights<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE>(P, M, N, p, d, time, st, c, Lo, park, unpark);
+            point_lights<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE, TwPark>(P, M, N, p, d, time, st, c, Lo, park, unpark);
         if (QUEUE && queued) {
             queue_write_lo(P, (long long)qtile * 64 + pix_lane(), Lo);
             *deferred = true;
