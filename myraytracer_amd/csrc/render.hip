@@ -474,8 +474,17 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             // eye - w*nd are computed once before the sample loop and spilled across the walks
             const int lane = pix_lane();
             const int ii = i0 + lane % kTileW, jj = j0 + lane / kTileW;
-            double nd = C.nd;
-            asm volatile("" : "+v"(nd));
+            // nd + 0 * sample index: a per-sample value (no fast-math, so not folded; the same
+            // value for every nd but -0).  An empty "+v" asm on nd instead made its VGPR copy once,
+            // in the prologue, and spilled it to scratch: 8 B per lane, 16.6 MB of HBM writes per
+            // C3 frame.
+            double nd;
+            if (!BOUNCE && !QUEUE && WALK == kWalkIdentity) {
+                nd = C.nd;
+                asm volatile("" : "+s"(nd));
+            } else {
+                nd = C.nd + 0.0 * (double)s;
+            }
             const double currentI = (double)ii + iOffset;
             const double currentJ = (double)jj + jOffset;
             const V3 vOff = v * (currentJ * C.dv);
