@@ -139,14 +139,14 @@ __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o
 template <bool COUNT, int WALK, bool WIDE, class WPark = TwParked, class Park, class Unpark>
 __device__ __forceinline__ void point_lights(const RenderParams& P, const DMaterial& M, const V3& N, const V3& p,
                                              const V3& d, double time, Stack& st, Counts& c, V3& Lo, Park park,
-                                             Unpark unpark) {
+                                             Unpark unpark, bool count_shadow = true) {
     for (int li = 0; li < P.num_plights; ++li) {
         const DPointLight& PL = P.plights[li];
         V3 wi = ld3(PL.position) - p;
         const double dist = length(wi);
         wi = normalize(wi);
         const V3 so = p + wi * P.shadow_eps;
-        c.shadow++;
+        if (count_shadow) c.shadow++;
         // The contribution is formed before the shadow walk (same expressions, same
         // values) so that only it - not N, wi, view, material - stays live across the walk.
         const double NdotL = smax(0.0, dot(N, wi));
@@ -340,7 +340,12 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
             const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && P.max_depth > 0;
             const unsigned long long m = __ballot(want);
             if (m) {
-                if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) P.bmask[qtile] = m;
+                // first active lane stores the mask and counts the wave's bounce rays: neither the
+                // lane id nor a per-lane counter stays live across the shadow walks
+                if (pix_lane() == __builtin_ctzll(__ballot(1))) {
+                    P.bmask[qtile] = m;
+                    atomicAdd(&P.counters[1], (unsigned long long)__builtin_popcountll(m));
+                }
                 if (want) {
                     const int l = pix_lane();                     // the lane's pixel, recomputed
                     const int i = i0 + l % kTileW, j = j0 + l / kTileW;
@@ -349,12 +354,17 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                     PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*pix_slot(3)),
                                             pixel_seed(i, j));
                     queue_write(P, q, M, d, N, p, r, time, i, j);
-                    c.secondary++;
                 }
             }
         }
+        if (QUEUE) {     // the wave counts its shadow rays here: no per-lane counter across the walks
+            const unsigned long long m = __ballot(computeDirect);
+            if (m && pix_lane() == __builtin_ctzll(__ballot(1)))
+                atomicAdd(&P.counters[0], (unsigned long long)__builtin_popcountll(m) * (unsigned)P.num_plights);
+        }
         if (computeDirect)
-            point_lights<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE, TwPark>(P, M, N, p, d, time, st, c, Lo, park, unpark);
+            point_lights<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE, TwPark>(P, M, N, p, d, time, st, c, Lo, park, unpark,
+                                                                          !QUEUE);
         if (QUEUE && queued) {
             queue_write_lo(P, (long long)qtile * 64 + pix_lane(), Lo);
             *deferred = true;
@@ -443,7 +453,10 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     // the tile's corner in VGPRs: the kernel's SGPRs are at the 106 limit, and uniform values
     // live across the walks there are spilled to VGPR lanes and restored with v_readlane
     int i0 = (tile % gx) * kTileW, j0 = chunk * 8;
-    asm volatile("" : "+v"(i0), "+v"(j0));
+    // (the queued pass keeps only the row there: both in VGPRs 6,061, neither 5,940, the row alone
+    // 6,152 Mrays/s on C5, profiles/r05v_ab_c5.txt)
+    if (!QUEUE) asm volatile("" : "+v"(i0), "+v"(j0));
+    else asm volatile("" : "+v"(j0));
     const DCamera& C = P.cam;
     Counts cnt{};
     bool valid;
