@@ -202,7 +202,8 @@ int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
  *   compact_records (1), compact_tris (1)   float32 records / triangles when exact
  *   xcd_group (0 = auto) tiles per XCD run      queue (1)  compacted bounce render (0 = megakernel)
  *   queue_levels (-1)    timing probe           hitlog (-1 = auto) logged hits per pixel
- *   nodeshade (1), levels (1), tree_ppw (4)     full trace() pass structure
+ *   nodeshade (1), levels (1), tree_ppw (4),
+ *   node_lists (1)                              full trace() pass structure
  *   full_flights (4)     full trace() renders overlapping on slot streams
  *   deep_cap_mb (8192)   deep trace() frames per launch batch
  *   batches (0 = auto), zerocopy (1)            rt_render delivery

@@ -242,6 +242,12 @@ struct RenderParams {
     int32_t tree_size;
     uint8_t* nflags;
     int32_t tree_ppw;                // node positions per wave in k_level / k_shade
+    // compacted node lists (render.hip k_clist; option compact): the flag-log entries a level pass
+    // or the node shading has work for, ascending; per-block counts; list lengths by word
+    // (level L: word L, node shading: word kCListShade)
+    uint32_t* clist;
+    uint32_t* cblk;
+    uint32_t* cword;
     // conservative FP32 four-wide walk (wide.h; identity scenes): nodes, the root node, the exact
     // FP64 box of every reference leaf by its first TriRec (6 doubles), the per-render widening of
     // every box (wdelta, world units: covers the FP32 rounding of o*inv for every ray origin of

@@ -826,6 +826,145 @@ __global__ void k_queue_reset(RenderParams P, int levels) {
         P.bmask[k] = 0ull;
     if (blockIdx.x == 0 && kQueueCount + (int)threadIdx.x < kCounterWords) P.counters[kQueueCount + threadIdx.x] = 0ull;
 }
+
+// ---- compacted node lists (option node_lists; render_full.h level / shading passes) ----------
+// k_level and k_shade give a wave one node position of a tile: a lane idles where its pixel's
+// trace() tree has no node there, and on C3g most do past level 0 (lane utilisation 0.34 / 0.41,
+// profiles/r04z_c3g_valu.txt).  Instead each pass after level 0 runs over a dense list of the
+// flag-log entries it has work for (flags holding `bits`), in the per-tile passes' order: by log
+// entry k, then 8x8 pixel tile, then pixel within the tile - a wave's lanes hold one node position
+// of 64 neighbouring pixels (row order instead of tiles measured 12 % slower node shading: lane
+// utilisation 0.36, profiles/r05x_shade_roofline.json).  The walks are the same (no PCG32 draw
+// inside these trees), only their assignment to lanes changes.
+// A level's entries are k = s per + first ... s per + first + width - 1 per traced sample s;
+// node shading takes every k.  Two passes over groups of 64 flags (one (k, tile) per thread):
+// k_ccount writes each block's count, k_clist prefixes the blocks before its own, writes the list
+// and its length.
+constexpr int kCListThreads = 256, kCListShade = 7;
+static_assert(kCListThreads == kQScanThreads, "block_sum_u64 sums kQScanThreads lanes");
+// the log entries [k_lo, k_hi) the groups of `level` run over (level < 0: the whole log)
+__host__ __device__ inline void clist_span(int tree, int per, int traced, int level, int& k_lo, int& k_hi) {
+    if (level < 0) { k_lo = 0; k_hi = traced * per; return; }
+    k_lo = tree_first(tree, level);
+    k_hi = (traced - 1) * per + tree_first(tree, level) + tree_width(tree, level);
+}
+__host__ __device__ inline int clist_tiles(int width, int num_chunks) { return num_chunks * ((width + 7) / 8); }
+// group g of `level`: its log entry k, tile row base q0 (row 0, column 0 of the tile) and the flags
+// of its 64 pixels holding `bits` (bit r * 8 + c: row r, column c of the tile)
+__device__ __forceinline__ unsigned long long clist_group(const RenderParams& P, size_t g, int level, unsigned bits,
+                                                          size_t& k, size_t& q0) {
+    const int W = P.cam.width, tiles = clist_tiles(W, P.num_chunks), gx = (W + 7) / 8;
+    int k_lo, k_hi;
+    clist_span(P.hit_tree, P.tree_size, P.hit_slots / P.tree_size, level, k_lo, k_hi);
+    k = (size_t)k_lo + g / (size_t)tiles;
+    const int t = (int)(g % (size_t)tiles), slot = t / gx, tx = t % gx;
+    q0 = (size_t)slot * 8 * W + (size_t)tx * 8;
+    if (k >= (size_t)k_hi) return 0ull;
+    if (level >= 0) {
+        const int h = (int)(k % (size_t)P.tree_size), first = tree_first(P.hit_tree, level);
+        if (h < first || h >= first + tree_width(P.hit_tree, level)) return 0ull;
+    }
+    const uint8_t* f = P.nflags + k * (size_t)P.hit_stride + q0;
+    unsigned long long m = 0;
+    if ((W & 7) == 0) {                                  // 8-byte aligned rows of the tile
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint2 v = *reinterpret_cast<const uint2*>(f + (size_t)r * W);
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if ((((c < 4 ? v.x : v.y) >> (8 * (c & 3))) & bits) == bits) m |= 1ull << (r * 8 + c);
+        }
+    } else {
+        const int cols = min(8, W - tx * 8);
+        for (int r = 0; r < 8; ++r)
+            for (int c = 0; c < cols; ++c)
+                if ((f[(size_t)r * W + c] & bits) == bits) m |= 1ull << (r * 8 + c);
+    }
+    return m;
+}
+__global__ __launch_bounds__(kCListThreads) void k_ccount(RenderParams P, int level, unsigned bits) {
+    __shared__ unsigned long long s_w[kCListThreads / 64];
+    size_t k, q0;
+    const size_t g = (size_t)blockIdx.x * kCListThreads + threadIdx.x;
+    const unsigned long long c = (unsigned long long)__popcll(clist_group(P, g, level, bits, k, q0));
+    const unsigned long long t = block_sum_u64(c, s_w);
+    if (threadIdx.x == 0) P.cblk[blockIdx.x] = (uint32_t)t;
+}
+__global__ __launch_bounds__(kCListThreads) void k_clist(RenderParams P, int level, unsigned bits, int word) {
+    __shared__ unsigned long long s_w[kCListThreads / 64];
+    const int t = threadIdx.x, lane = t & 63;
+    unsigned long long before = 0;                       // the blocks before this one
+    for (int b = t; b < (int)blockIdx.x; b += kCListThreads) before += P.cblk[b];
+    before = block_sum_u64(before, s_w);
+    size_t k, q0;
+    const size_t g = (size_t)blockIdx.x * kCListThreads + t;
+    unsigned long long m = clist_group(P, g, level, bits, k, q0);
+    const unsigned mine = (unsigned)__popcll(m);
+    unsigned inc = mine;                                 // inclusive scan over the wave, then the block
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned y = (unsigned)__shfl_up((int)inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_w[t >> 6] = inc;
+    __syncthreads();
+    unsigned at = (unsigned)before + inc - mine;
+    for (int w = 0; w < (t >> 6); ++w) at += (unsigned)s_w[w];
+    const unsigned end = at + mine;
+    const size_t base = k * (size_t)P.hit_stride + q0;
+    const int W = P.cam.width;
+    while (m) {
+        const int b = __builtin_ctzll(m);
+        P.clist[at++] = (uint32_t)(base + (size_t)(b >> 3) * W + (b & 7));
+        m &= m - 1ull;
+    }
+    if (blockIdx.x == gridDim.x - 1 && t == kCListThreads - 1) P.cword[word] = end;
+}
+
+// Level `level` (>= 1) over its list: one lane per existing node (level_node, as k_level).  A
+// fixed grid of waves strides over the list in batches of 64 (its length is on the device).
+template <int WALK>
+__global__ __launch_bounds__(64) MYRT_FULL_ATTR void k_level_c(RenderParams P, int level) {
+    extern __shared__ unsigned long long lds_stack[];
+    const unsigned T = P.cword[level];
+    const unsigned S = (unsigned)P.hit_stride, per = (unsigned)P.tree_size;
+    const unsigned lane = threadIdx.x & 63;
+    Counts cnt{};
+    MYRT_STACK(st, lds_stack);
+    for (unsigned x0 = blockIdx.x * 64u; x0 < T; x0 += gridDim.x * 64u) {
+        if (x0 + lane < T) {
+            const unsigned at = P.clist[x0 + lane];
+            const unsigned k = at / S, q = at - k * S, s = k / per;
+            const DNodeRec n = P.nodes[at];
+            level_node<WALK>(P, q, (int)s, (int)(k - s * per), level, v3(n.o[0], n.o[1], n.o[2]),
+                             v3(n.d[0], n.d[1], n.d[2]), 0.0, n.time, st, cnt);
+        }
+    }
+    flush_ties(P, cnt);
+}
+
+// Node shading over its list: one lane per logged walk that hit (shade_node, as k_shade).
+template <int WALK>
+__global__ __launch_bounds__(64) MYRT_FULL_ATTR void k_shade_c(RenderParams P) {
+    extern __shared__ unsigned long long lds_stack[];
+    const unsigned T = P.cword[kCListShade];
+    const unsigned S = (unsigned)P.hit_stride;
+    const unsigned lane = threadIdx.x & 63;
+    Counts cnt{};
+    MYRT_STACK(st, lds_stack);
+    for (unsigned x0 = blockIdx.x * 64u; x0 < T; x0 += gridDim.x * 64u) {
+        if (x0 + lane < T) {
+            const unsigned at = P.clist[x0 + lane];
+            const unsigned k = at / S;
+            shade_node<WALK>(P, at - k * S, (int)k, st, cnt);
+        }
+    }
+    const unsigned long long s0 = wave_sum(cnt.shadow), s2 = wave_sum(cnt.shadow_traced);
+    if (lane == 0) {
+        if (s0) atomicAdd(&P.counters[0], s0);
+        if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
+    }
+}
 }  // namespace dev
 }  // namespace myrt
 
@@ -926,9 +1065,12 @@ struct FullScratch {
     int64_t nodes_cap = 0, walks_cap = 0;     // records (nodes, node_lo); pixels (walks)
     uint8_t* nflags = nullptr;                // level passes: per-node flags
     int64_t nflags_cap = 0;
+    uint32_t* clist = nullptr;                // compacted node lists: entries, then block counts,
+    int64_t clist_cap = 0;                    // then 8 list lengths (k_clist)
     void release() {
         (void)hipFree(events); (void)hipFree(jstart); (void)hipFree(hitlog);
         (void)hipFree(nodes); (void)hipFree(node_lo); (void)hipFree(walks); (void)hipFree(nflags);
+        (void)hipFree(clist);
         *this = FullScratch{};
     }
 };
@@ -1002,7 +1144,7 @@ enum OptId {
     kOptWide, kOptUnified, kOptUnifiedTransformed, kOptCompactRecords, kOptCompactTris, kOptXcdGroup,
     kOptQueue, kOptQueueLevels, kOptHitlog, kOptNodeshade, kOptLevels, kOptTreePpw, kOptFullFlights,
     kOptDeepCapMb, kOptBatches, kOptZerocopy, kOptSubmitEvents, kOptSubmitCounters, kOptSubmitDma,
-    kOptDebugFailReplica, kOptWideDeltaScale, kOptCount
+    kOptDebugFailReplica, kOptWideDeltaScale, kOptNodeLists, kOptCount
 };
 struct OptDef { const char* name; int64_t def, lo, hi; };
 static const OptDef kOptDefs[kOptCount] = {
@@ -1029,6 +1171,7 @@ static const OptDef kOptDefs[kOptCount] = {
     {"wide_delta_scale", 1000, 0, 1000000},    // test hook: the four-wide walk's widening (wdelta) in
                                                // 1/1000 of the exact bound; < 1000 voids wide.h's
                                                // exactness proof (tests show that it has teeth)
+    {"node_lists", 1, 0, 1},              // level passes past 0 and node shading over compacted node lists
 };
 
 struct rt_scene {
@@ -1438,6 +1581,16 @@ static int64_t hit_slots_for(const RenderParams& P, bool dielectric, int64_t px)
     const int64_t by_mem = kHitLogBytes / std::max<int64_t>(1, px * (int64_t)(sizeof(DHitRec) + sizeof(DNodeRec) + 24));
     return std::max<int64_t>(0, std::min<int64_t>({per_sample * traced, 64, by_mem}));
 }
+// The list of level `level`'s entries (level < 0: every logged walk) whose flags hold `bits`,
+// its length into list word `word` (render.hip k_ccount / k_clist).
+static void clist_launch(const RenderParams& P, int level, unsigned bits, int word, hipStream_t stream) {
+    int k_lo, k_hi;
+    dev::clist_span(P.hit_tree, P.tree_size, P.hit_slots / P.tree_size, level, k_lo, k_hi);
+    const unsigned long long groups = (unsigned long long)(k_hi - k_lo) * dev::clist_tiles(P.cam.width, P.num_chunks);
+    const dim3 grid((unsigned)((groups + dev::kCListThreads - 1) / dev::kCListThreads));
+    hipLaunchKernelGGL(dev::k_ccount, grid, dim3(dev::kCListThreads), 0, stream, P, level, bits);
+    hipLaunchKernelGGL(dev::k_clist, grid, dim3(dev::kCListThreads), 0, stream, P, level, bits, word);
+}
 static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs, RenderParams P, hipStream_t stream,
                            bool count, bool dielectric, bool rough) {
     const int bt = kRenderBlock;
@@ -1472,6 +1625,10 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
     // area lights take the same level passes + node shading when they apply (no rough
     // material, whole trees logged), else render_full alone walks and shades every tree.
     const bool alights = P.num_alights > 0;
+    bool lists = false;                       // compacted node lists (k_level_c / k_shade_c)
+    // their passes: a fixed grid of one-wave blocks striding over the list
+    const dim3 cgrid((unsigned)(r.cus * 4 * 4));
+    const size_t clds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
     if (alights || (dielectric && !count && !deep)) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
         if (px > fs.cap_px) {
@@ -1543,6 +1700,21 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
             else (void)hipGetLastError();             // depth-first k_events
         }
         levels = levels && slots * px <= fs.nflags_cap && px <= fs.cap_px;
+        // compacted node lists: entry indices are u32; list + block counts + lengths
+        const int64_t cgroups = slots * dev::clist_tiles(P.cam.width, P.num_chunks);
+        const int64_t cblocks = (cgroups + dev::kCListThreads - 1) / dev::kCListThreads;
+        const int64_t cwords = slots * px + cblocks + 8;
+        lists = levels && s->opt[kOptNodeLists] != 0 && slots * px < (int64_t(1) << 32);
+        if (lists && cwords > fs.clist_cap) {
+            retire(r, fs.clist);
+            fs.clist = nullptr; fs.clist_cap = 0;
+            if (hipMalloc((void**)&fs.clist, (size_t)cwords * sizeof(uint32_t)) == hipSuccess) fs.clist_cap = cwords;
+            else (void)hipGetLastError();             // the per-tile passes
+        }
+        lists = lists && cwords <= fs.clist_cap;
+        P.clist = lists ? fs.clist : nullptr;
+        P.cblk = lists ? fs.clist + slots * px : nullptr;
+        P.cword = lists ? fs.clist + slots * px + cblocks : nullptr;
         if (!alights && !levels) {                     // dielectrics only: render_full does it all
             P.hits = nullptr; P.hit_slots = 0;
             P.nodes = nullptr; P.node_lo = nullptr; P.walks = nullptr;
@@ -1557,11 +1729,18 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
             P.slot_base = 0;
             const unsigned g0 = per_slot * (unsigned)P.num_chunks;
 #define MYRT_LV(W_) hipLaunchKernelGGL((dev::k_level<W_>), dim3(g0, ly, 1), block, lds, stream, P, level)
+#define MYRT_LVC(W_) hipLaunchKernelGGL((dev::k_level_c<W_>), cgrid, dim3(64), clds, stream, P, level)
             for (int32_t level = 0; level <= P.max_depth; ++level) {
+                if (lists && level > 0) {
+                    clist_launch(P, level, dev::kNodeExists, level, stream);
+                    MYRT_BY_WALK(MYRT_LVC);
+                    continue;
+                }
                 const unsigned ly = level == 0 ? 1u : (unsigned)(traced * dev::tree_rows(tree, level, P.tree_ppw));
                 MYRT_BY_WALK(MYRT_LV);
             }
 #undef MYRT_LV
+#undef MYRT_LVC
             hipLaunchKernelGGL(dev::k_jofs, dim3(g0), block, 0, stream, P);
         }
         for (int32_t base = 0; base < P.num_chunks && !levels && alights; base += batch) {
@@ -1582,8 +1761,15 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
             const dim3 sgrid(per_slot * (unsigned)P.num_chunks,
                              P.hit_tree ? (unsigned)(traced * shade_rows) : (unsigned)slots, 1);
 #define MYRT_SH(W_) hipLaunchKernelGGL((dev::k_shade<W_>), sgrid, block, lds, stream, P)
-            MYRT_BY_WALK(MYRT_SH);
+#define MYRT_SHC(W_) hipLaunchKernelGGL((dev::k_shade_c<W_>), cgrid, dim3(64), clds, stream, P)
+            if (lists) {
+                clist_launch(P, -1, dev::kNodeHit, dev::kCListShade, stream);
+                MYRT_BY_WALK(MYRT_SHC);
+            } else {
+                MYRT_BY_WALK(MYRT_SH);
+            }
 #undef MYRT_SH
+#undef MYRT_SHC
         }
     }
     for (int32_t base = 0; base < P.num_chunks; base += batch) {

@@ -157,7 +157,7 @@ struct HitLog {
     int k, cap;
     int tree = 0, node = 0, sbase = 0;
 };
-enum : uint8_t { kNodeExists = 1, kNodeEval = 2 };
+enum : uint8_t { kNodeExists = 1, kNodeEval = 2, kNodeHit = 4 };
 __device__ __forceinline__ int tree_child(int b, int h, int which) { return b == 2 ? 2 * h + 1 + which : h + 1; }
 __device__ __forceinline__ int tree_parent(int b, int h) { return b == 2 ? (h - 1) >> 1 : h - 1; }
 // Level L of a tree: its first node and its width; a wave runs up to P.tree_ppw of its node
@@ -466,6 +466,7 @@ __device__ __forceinline__ void level_node(const RenderParams& P, size_t q, int 
     P.hits[at] = r;
     uint8_t fl = kNodeExists;
     if (hh.inst >= 0) {
+        fl |= kNodeHit;
         V3 p, Ngeo;
         hit_geometry<false>(P, o, d, time, hh, p, Ngeo, c);
         const DMaterial& M = P.mats[max(0, min(P.num_mats - 1, P.insts[hh.inst].material - 1))];

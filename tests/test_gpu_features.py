@@ -136,35 +136,38 @@ def test_area_light_hit_log(slots, nodeshade):
     assert st.secondary_rays > 0
 
 
-@pytest.mark.parametrize("levels, ppw", [(1, 4), (1, 1), (1, 64), (0, 4)])
+@pytest.mark.parametrize("levels, ppw, lists", [(1, 4, 1), (1, 4, 0), (1, 1, 0), (1, 64, 0), (0, 4, 1)])
 @pytest.mark.parametrize("spp, depth, glass", [(1, 4, True), (4, 3, True), (1, 5, True), (4, 4, False), (9, 2, True)])
-def test_area_light_level_passes(levels, ppw, spp, depth, glass):
+def test_area_light_level_passes(levels, ppw, lists, spp, depth, glass):
     """Breadth-first events passes (render_full.h k_level, option levels = 1, default) against the
     depth-first k_events (0): no rough material, so the tree's walks may run level by level;
     heap-indexed trees with glass (2^(D+1) - 1 nodes per traced sample), chains without; 4 and 9
     samples per pixel give several trees per pixel; depth 5 with one sample fills 63 of the 64
-    log slots.  k_jofs must reproduce the depth-first jitterIndex offsets exactly.  A wave runs 1,
-    4 (default) or all of a level's node positions (option tree_ppw)."""
-    sc = _area_scene(72, 56, spp=spp)
+    log slots.  k_jofs must reproduce the depth-first jitterIndex offsets exactly.  Levels past 0
+    and the node shading run over compacted node lists (option node_lists = 1, default: k_clist,
+    k_level_c, k_shade_c; several traced samples give a level several spans of the log) or per
+    tile, a wave running 1, 4 (default) or all of a level's node positions (option tree_ppw)."""
+    sc = _area_scene(70, 56, spp=spp)                   # width 70: ragged last tile column
     sc.objects[1].material = "3" if glass else "2"
     sc.objects[2].material = "4"
     sc.objects[3].material = "3" if glass else "4"
     sc.max_recursion_depth = depth
-    st = _compare(sc, options={"levels": levels, "tree_ppw": ppw})
+    st = _compare(sc, options={"levels": levels, "tree_ppw": ppw, "node_lists": lists})
     assert st.secondary_rays > 0
 
 
-@pytest.mark.parametrize("levels", [1, 0])
+@pytest.mark.parametrize("levels, lists", [(1, 1), (1, 0), (0, 1)])
 @pytest.mark.parametrize("spp, depth", [(1, 4), (4, 3)])
-def test_dielectric_level_passes_without_area_lights(levels, spp, depth):
+def test_dielectric_level_passes_without_area_lights(levels, lists, spp, depth):
     """Glass + mirror + conductor with point lights only: the level passes and node shading
-    (option levels = 1, default) or render_full alone (0).  No jitterIndex here, so no events prefix."""
+    (option levels = 1, default; over compacted node lists or per tile, option node_lists) or
+    render_full alone (levels = 0).  No jitterIndex here, so no events prefix."""
     sc = _primitives_scene(80, 60)
     sc.cameras[0].num_samples = spp
     sc.objects[1].material = "3"
     sc.objects[3].material = "3"
     sc.max_recursion_depth = depth
-    st = _compare(sc, options={"levels": levels})
+    st = _compare(sc, options={"levels": levels, "node_lists": lists})
     assert st.secondary_rays > 0
 
 
