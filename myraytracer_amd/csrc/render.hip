@@ -846,11 +846,12 @@ __global__ void k_queue_reset(RenderParams P, int levels) {
 // and its length.
 constexpr int kCListThreads = 256, kCListShade = 7;
 static_assert(kCListThreads == kQScanThreads, "block_sum_u64 sums kQScanThreads lanes");
-// the log entries [k_lo, k_hi) the groups of `level` run over (level < 0: the whole log)
-__host__ __device__ inline void clist_span(int tree, int per, int traced, int level, int& k_lo, int& k_hi) {
-    if (level < 0) { k_lo = 0; k_hi = traced * per; return; }
+// the log entries [k_lo, k_hi) the groups of `level` run over (level < 0: the whole log, also
+// k_events' walk-indexed log: tree 0)
+__host__ __device__ inline void clist_span(int tree, int per, int slots, int level, int& k_lo, int& k_hi) {
+    if (level < 0) { k_lo = 0; k_hi = slots; return; }
     k_lo = tree_first(tree, level);
-    k_hi = (traced - 1) * per + tree_first(tree, level) + tree_width(tree, level);
+    k_hi = (slots / per - 1) * per + tree_first(tree, level) + tree_width(tree, level);
 }
 __host__ __device__ inline int clist_tiles(int width, int num_chunks) { return num_chunks * ((width + 7) / 8); }
 // group g of `level`: its log entry k, tile row base q0 (row 0, column 0 of the tile) and the flags
@@ -859,7 +860,7 @@ __device__ __forceinline__ unsigned long long clist_group(const RenderParams& P,
                                                           size_t& k, size_t& q0) {
     const int W = P.cam.width, tiles = clist_tiles(W, P.num_chunks), gx = (W + 7) / 8;
     int k_lo, k_hi;
-    clist_span(P.hit_tree, P.tree_size, P.hit_slots / P.tree_size, level, k_lo, k_hi);
+    clist_span(P.hit_tree, P.tree_size, P.hit_slots, level, k_lo, k_hi);
     k = (size_t)k_lo + g / (size_t)tiles;
     const int t = (int)(g % (size_t)tiles), slot = t / gx, tx = t % gx;
     q0 = (size_t)slot * 8 * W + (size_t)tx * 8;
@@ -1589,7 +1590,7 @@ static int64_t hit_slots_for(const RenderParams& P, bool dielectric, int64_t px)
 // its length into list word `word` (render.hip k_ccount / k_clist).
 static void clist_launch(const RenderParams& P, int level, unsigned bits, int word, hipStream_t stream) {
     int k_lo, k_hi;
-    dev::clist_span(P.hit_tree, P.tree_size, P.hit_slots / P.tree_size, level, k_lo, k_hi);
+    dev::clist_span(P.hit_tree, P.tree_size, P.hit_slots, level, k_lo, k_hi);
     const unsigned long long groups = (unsigned long long)(k_hi - k_lo) * dev::clist_tiles(P.cam.width, P.num_chunks);
     const dim3 grid((unsigned)((groups + dev::kCListThreads - 1) / dev::kCListThreads));
     hipLaunchKernelGGL(dev::k_ccount, grid, dim3(dev::kCListThreads), 0, stream, P, level, bits);
@@ -1697,18 +1698,23 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
                                       ? (tree == 2 ? (int64_t(2) << P.max_depth) - 1 : P.max_depth + 1) : 0;
         bool levels = nodeshade && !deep && P.has_tlas && tree_size > 0 && slots == tree_size * traced &&
                       !rough && s->opt[kOptLevels] != 0;
-        if (levels && slots * px > fs.nflags_cap) {
+        // node lists (option node_lists): over the level passes' flags, or - depth-first k_events
+        // with area lights - over hit flags k_events writes for node shading
+        const bool want_lists = nodeshade && s->opt[kOptNodeLists] != 0 && slots * px < (int64_t(1) << 32);
+        bool flags_ev = want_lists && !levels && alights;
+        if ((levels || flags_ev) && slots * px > fs.nflags_cap) {
             retire(r, fs.nflags);
             fs.nflags = nullptr; fs.nflags_cap = 0;
             if (hipMalloc((void**)&fs.nflags, (size_t)(slots * px)) == hipSuccess) fs.nflags_cap = slots * px;
             else (void)hipGetLastError();             // depth-first k_events
         }
         levels = levels && slots * px <= fs.nflags_cap && px <= fs.cap_px;
+        flags_ev = flags_ev && slots * px <= fs.nflags_cap;
         // compacted node lists: entry indices are u32; list + block counts + lengths
         const int64_t cgroups = slots * dev::clist_tiles(P.cam.width, P.num_chunks);
         const int64_t cblocks = (cgroups + dev::kCListThreads - 1) / dev::kCListThreads;
         const int64_t cwords = slots * px + cblocks + 8;
-        lists = levels && s->opt[kOptNodeLists] != 0 && slots * px < (int64_t(1) << 32);
+        lists = want_lists && (levels || flags_ev);
         if (lists && cwords > fs.clist_cap) {
             retire(r, fs.clist);
             fs.clist = nullptr; fs.clist_cap = 0;
@@ -1727,7 +1733,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         P.hit_tree = levels ? tree : 0;
         P.tree_ppw = (int32_t)s->opt[kOptTreePpw];
         P.tree_size = levels ? (int32_t)tree_size : 0;
-        P.nflags = levels ? fs.nflags : nullptr;
+        P.nflags = (levels || lists) ? fs.nflags : nullptr;
+        if (lists && !levels) HIP_TRY(hipMemsetAsync(fs.nflags, 0, (size_t)(slots * px), stream));
         if (levels) {
             HIP_TRY(hipMemsetAsync(fs.nflags, 0, (size_t)(slots * px), stream));
             P.slot_base = 0;

@@ -204,6 +204,8 @@ __device__ V3 trace_full(const RenderParams& P, V3 o, V3 d, double tlo, double t
                         n.jofs = (int32_t)jitterIndex;
                         n.hit = h.inst >= 0 ? 1 : 0;
                         P.nodes[(size_t)hl.k * hl.stride + (size_t)(hl.p - P.hits)] = n;
+                        // node lists (render.hip k_clist): the walks k_shade_c shades
+                        if (P.nflags && h.inst >= 0) P.nflags[(size_t)hl.k * hl.stride + (size_t)(hl.p - P.hits)] = kNodeHit;
                     }
                 }
             }

@@ -118,13 +118,16 @@ def test_area_lights_with_dielectric_and_mesh():
     _compare(sc)
 
 
-@pytest.mark.parametrize("slots, nodeshade", [(-1, 1), (-1, 0), (1, 1), (8, 1), (0, 1)])
-def test_area_light_hit_log(slots, nodeshade):
+@pytest.mark.parametrize("slots, nodeshade, lists", [(-1, 1, 1), (-1, 1, 0), (-1, 0, 1), (1, 1, 1), (8, 1, 1),
+                                                     (0, 1, 1)])
+def test_area_light_hit_log(slots, nodeshade, lists):
     """render_full reads the closest hits k_events logged instead of walking them again
     (RenderParams::hits), and k_shade shades the logged hits node-parallel (option nodeshade = 1,
     default) or render_full does (0): the default log holds every walk of the paths here, 8 or
     1 slots send longer paths past the log to the fallback walk, 0 turns the log off.  Glass, mirror and a rough
-    dielectric give paths of up to 2^5 - 1 walks; four samples per pixel."""
+    dielectric give paths of up to 2^5 - 1 walks; four samples per pixel.  The rough material keeps
+    the depth-first k_events: node shading runs over the list of logged hits it flags (option
+    node_lists = 1, default) or per (tile, walk)."""
     # hitlog -1: sized to the scene's path trees (here 31 per sample); nodeshade: logged hits shaded
     # node-parallel (k_shade) or by render_full
     sc = _area_scene(88, 64, spp=4)
@@ -132,7 +135,7 @@ def test_area_light_hit_log(slots, nodeshade):
     sc.objects[2].material = "2"
     sc.objects[3].material = "5"
     sc.max_recursion_depth = 4
-    st = _compare(sc, options={"hitlog": slots, "nodeshade": nodeshade})
+    st = _compare(sc, options={"hitlog": slots, "nodeshade": nodeshade, "node_lists": lists})
     assert st.secondary_rays > 0
 
 
