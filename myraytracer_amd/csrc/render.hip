@@ -928,8 +928,12 @@ __global__ __launch_bounds__(kCListThreads) void k_clist(RenderParams P, int lev
 
 // Level `level` (>= 1) over its list: one lane per existing node (level_node, as k_level).  A
 // fixed grid of waves strides over the list in batches of 64 (its length is on the device).
+#ifndef MYRT_LEVELC_WPE
+#define MYRT_LEVELC_WPE 4   // waves/SIMD of k_level_c (grid: cus x 4 x MYRT_LEVELC_WPE)
+#endif
 template <int WALK>
-__global__ __launch_bounds__(64) MYRT_FULL_ATTR void k_level_c(RenderParams P, int level) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_LEVELC_WPE))) void k_level_c(RenderParams P,
+                                                                                                   int level) {
     extern __shared__ unsigned long long lds_stack[];
     const unsigned T = P.cword[level];
     const unsigned S = (unsigned)P.hit_stride, per = (unsigned)P.tree_size;
@@ -949,8 +953,13 @@ __global__ __launch_bounds__(64) MYRT_FULL_ATTR void k_level_c(RenderParams P, i
 }
 
 // Node shading over its list: one lane per logged walk that hit (shade_node, as k_shade).
+#ifndef MYRT_SHADE_WPE
+#define MYRT_SHADE_WPE 5    // waves/SIMD of k_shade_c (its grid fills them: cus x 4 x MYRT_SHADE_WPE);
+                            // 5 with 36 VGPR spills beat 4 without: C3g 3.22 -> 3.14 ms per frame,
+                            // C3r 3.78 -> 3.74 (6: 3.21 / 3.77; profiles/r05zc_ab_c3{g,r}.txt)
+#endif
 template <int WALK>
-__global__ __launch_bounds__(64) MYRT_FULL_ATTR void k_shade_c(RenderParams P) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_SHADE_WPE))) void k_shade_c(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     const unsigned T = P.cword[kCListShade];
     const unsigned S = (unsigned)P.hit_stride;
@@ -1631,8 +1640,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
     // material, whole trees logged), else render_full alone walks and shades every tree.
     const bool alights = P.num_alights > 0;
     bool lists = false;                       // compacted node lists (k_level_c / k_shade_c)
-    // their passes: a fixed grid of one-wave blocks striding over the list
-    const dim3 cgrid((unsigned)(r.cus * 4 * 4));
+    // their passes: a fixed grid of one-wave blocks striding over the list, one block per wave
+    // slot of the chip at the kernel's occupancy (MYRT_LEVELC_WPE, MYRT_SHADE_WPE)
     const size_t clds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
     if (alights || (dielectric && !count && !deep)) {
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
@@ -1740,7 +1749,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
             P.slot_base = 0;
             const unsigned g0 = per_slot * (unsigned)P.num_chunks;
 #define MYRT_LV(W_) hipLaunchKernelGGL((dev::k_level<W_>), dim3(g0, ly, 1), block, lds, stream, P, level)
-#define MYRT_LVC(W_) hipLaunchKernelGGL((dev::k_level_c<W_>), cgrid, dim3(64), clds, stream, P, level)
+#define MYRT_LVC(W_) hipLaunchKernelGGL((dev::k_level_c<W_>), dim3((unsigned)(r.cus * 4 * MYRT_LEVELC_WPE)), dim3(64), clds, stream, P, level)
             for (int32_t level = 0; level <= P.max_depth; ++level) {
                 if (lists && level > 0) {
                     clist_launch(P, level, dev::kNodeExists, level, stream);
@@ -1772,7 +1781,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
             const dim3 sgrid(per_slot * (unsigned)P.num_chunks,
                              P.hit_tree ? (unsigned)(traced * shade_rows) : (unsigned)slots, 1);
 #define MYRT_SH(W_) hipLaunchKernelGGL((dev::k_shade<W_>), sgrid, block, lds, stream, P)
-#define MYRT_SHC(W_) hipLaunchKernelGGL((dev::k_shade_c<W_>), cgrid, dim3(64), clds, stream, P)
+#define MYRT_SHC(W_) hipLaunchKernelGGL((dev::k_shade_c<W_>), dim3((unsigned)(r.cus * 4 * MYRT_SHADE_WPE)), dim3(64), clds, stream, P)
             if (lists) {
                 clist_launch(P, -1, dev::kNodeHit, dev::kCListShade, stream);
                 MYRT_BY_WALK(MYRT_SHC);
