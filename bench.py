@@ -333,13 +333,14 @@ def main():
     staged = strong and world > 1 and args.gather == "staged"
     my_rows = None
     if strong and world > 1:
-        mine_rows = np.concatenate([np.arange(8 * c, min(8 * c + 8, H)) for c in range(first, (H + 7) // 8, step)])
         for q in range(Q):
             sf = SharedFrame(W * H * 4, rank, world, dist, f"{args.config}{q}")
             shared.append(sf)
         if args.numa_placement == "first-touch" and not staged:
             # every rank first-touches its own rows (8-row chunks c = rank mod world) while bound to
             # its GPU's node; registration (which faults every page it touches first) waits for all
+            mine_rows = np.concatenate([np.arange(8 * c, min(8 * c + 8, H))
+                                        for c in range(first, (H + 7) // 8, step)] or [np.empty(0, np.int64)])
             for sf in shared:
                 sf.array.reshape(H, W, 4)[mine_rows] = 0
             dist.barrier()
@@ -353,7 +354,8 @@ def main():
             fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
             for fb_ in fbs:
                 fb_[:] = 0
-            my_rows = np.concatenate([np.arange(8 * c, min(8 * c + 8, H)) for c in range(first, (H + 7) // 8, step)])
+            my_rows = np.concatenate([np.arange(8 * c, min(8 * c + 8, H))
+                                      for c in range(first, (H + 7) // 8, step)] or [np.empty(0, np.int64)])
             eng.set_option("submit_dma", 1)
         else:
             fbs = gathered

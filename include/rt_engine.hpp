@@ -135,6 +135,10 @@ public:
 
     /* Render options (rt_scene_set_option; defaults are the production settings). */
     void setOption(const std::string& name, int64_t value) { check(rt_scene_set_option(scene_, name.c_str(), value)); }
+    /* Test hooks (rt_scene_set_unsafe_option: not for production, rtcore.h). */
+    void setUnsafeOption(const std::string& name, int64_t value) {
+        check(rt_scene_set_unsafe_option(scene_, name.c_str(), value));
+    }
     int64_t option(const std::string& name) const {
         int64_t v = 0;
         check(rt_scene_get_option(scene_, name.c_str(), &v));

@@ -47,8 +47,10 @@
  *      RT_ERR_INVALID_ARG instead of an unchecked read.
  *   3: rt_stats gained `rewalked` and rt_scene_info `scratch_bytes` (both appended: the
  *      structs grew); rt_scene_set_option / rt_scene_get_option replace the MYRT_*
- *      environment switches (the library reads no environment variable on the render path). */
-#define RT_ABI_VERSION 3
+ *      environment switches (the library reads no environment variable on the render path).
+ *   4: the test hooks debug_fail_replica / wide_delta_scale moved behind the non-production
+ *      rt_scene_set_unsafe_option; rt_scene_set_option refuses them. */
+#define RT_ABI_VERSION 4
 
 #ifdef __cplusplus
 extern "C" {
@@ -208,13 +210,19 @@ int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
  *   deep_cap_mb (8192)   deep trace() frames per launch batch
  *   batches (0 = auto), zerocopy (1)            rt_render delivery
  *   submit_events (1), submit_counters (1), submit_dma (0)   rt_render_submit delivery
- *   debug_fail_replica (-1)   test hook: inject a launch failure on that replica
- *   wide_delta_scale (1000)   test hook: the four-wide walk's widening in 1/1000 of the proven
- *                             bound (wide.h); below 1000 exactness is no longer guaranteed
  * Unknown names and out-of-range values return RT_ERR_INVALID_ARG.  Set options between
- * renders (not while renders of the scene are in flight). */
+ * renders (not while renders of the scene are in flight).  The test hooks below are refused
+ * here (RT_ERR_INVALID_ARG); rt_scene_get_option reads every option. */
 int32_t rt_scene_set_option(rt_scene* scene, const char* name, int64_t value);
 int32_t rt_scene_get_option(const rt_scene* scene, const char* name, int64_t* value);
+
+/* NOT FOR PRODUCTION (ABI 4).  Sets any option, including the test hooks that
+ * rt_scene_set_option refuses because they void the library's guarantees:
+ *   debug_fail_replica (-1)   inject a launch failure on that replica
+ *   wide_delta_scale (1000)   the four-wide walk's widening in 1/1000 of the proven bound
+ *                             (wide.h); below 1000 exactness is no longer guaranteed
+ * Used only by the parity tests that show the exactness proof has teeth. */
+int32_t rt_scene_set_unsafe_option(rt_scene* scene, const char* name, int64_t value);
 
 /* ---- rendering -------------------------------------------------------------- */
 /* Renders 8-row chunks chunk_first, chunk_first+chunk_step, ... of camera

@@ -131,8 +131,9 @@ EXPORTED_SYMBOLS = [
     "rt_render_ex", "rt_host_register", "rt_host_unregister",
     "rt_scene_file_load", "rt_scene_file_parse", "rt_scene_file_desc", "rt_scene_file_image_name",
     "rt_scene_file_last_error", "rt_scene_file_destroy", "rt_scene_set_option", "rt_scene_get_option",
+    "rt_scene_set_unsafe_option",
 ]
-RT_ABI_VERSION = 3
+RT_ABI_VERSION = 4
 
 
 def bind(lib: C.CDLL) -> C.CDLL:
@@ -213,4 +214,7 @@ def bind(lib: C.CDLL) -> C.CDLL:
         lib.rt_scene_set_option.restype = C.c_int32
         lib.rt_scene_get_option.argtypes = [C.c_void_p, C.c_char_p, P(C.c_int64)]
         lib.rt_scene_get_option.restype = C.c_int32
+    if hasattr(lib, "rt_scene_set_unsafe_option"):   # ABI >= 4 (test hooks, not for production)
+        lib.rt_scene_set_unsafe_option.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+        lib.rt_scene_set_unsafe_option.restype = C.c_int32
     return lib

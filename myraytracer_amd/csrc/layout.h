@@ -140,15 +140,17 @@ struct DNodeRec { double o[3], d[3], time; int32_t jofs, hit; };
 // A queued mirror/conductor bounce ray (compacted bounce render, render.hip k_bounce): the
 // child trace(depth + 1) of one sample plus what its parent level adds back,
 // Lo_parent + M_parent * trace(depth + 1) (Object+Extension.swift:189-206, 252-275).
-// The level-k record of a pixel sits at [(k - 1) * cap + pixel slot] of RenderParams::bounce,
-// so its parent is the same slot one level up.
+// Records are compacted per level (render.hip q_reserve: a level holds only its rays); `parent`
+// is the index of the record one level up (-1 at level 1), so a ray that ends resolves its sample
+// backward along the parents.
 struct alignas(128) BounceRec {
     double o[3], d[3];        // the reflected ray (origin p + N * shadowRayEpsilon, tMin 0)
     double Lo[3], M[3];       // the parent level's radiance and its mirror/Fresnel multiplier
     unsigned long long rng;   // the sample's PCG32 state after the parent's draws (roughness)
     double time;              // the sample's ray time (instance motion)
     int32_t i, j;             // pixel
-    int32_t pad[2];
+    int32_t parent;           // the parent level's record (index into RenderParams::bounce), -1 at level 1
+    int32_t pad;
 };
 static_assert(sizeof(BounceRec) == 128, "BounceRec is one 128-B line");
 
@@ -206,15 +208,15 @@ struct RenderParams {
     void* deep;
     int32_t slot_base;
     // compacted bounce render (render.hip k_bounce); bounce == nullptr: the bounce megakernel.
-    // Ray records by pixel slot: [level - 1][tile * 64 + lane] (tile = wave of the primary launch);
-    // bmask[level - 1][tile] = the tile's lanes with a ray at that level; bact = k_qscan's list of
-    // the level's tiles that have rays ([0, A) tile ids, [bounce_tiles, bounce_tiles + A) the
-    // exclusive prefix of their ray counts)
+    // Level L's rays sit in kQRegions regions of qhdr[kQHdrCap + L] records from record qhdr[L]
+    // on; region r's count is the counter q_counter(L, r) (wave-level atomic reservation,
+    // q_reserve).  qneed (host-mapped, or null): each level's largest region count, written by
+    // k_queue_done, so the host can grow the arena and render an overflowed frame again.
     BounceRec* bounce;
-    unsigned long long* bmask;
-    uint32_t* bact;
-    int64_t bounce_cap;              // records per level = bounce_tiles * 64
-    int32_t bounce_tiles;
+    unsigned long long* qhdr;
+    unsigned long long* qneed;
+    int64_t qrecs;                   // records in the arena
+    int32_t qlevels;                 // levels the arena holds
     double* out_rgb;                 // packed rows of the selected chunks
     uint8_t* out_rgba8;
     unsigned long long* counters;    // [0] shadow rays cast, [1] secondary rays, [2..12] work counters,
@@ -265,14 +267,22 @@ struct RenderParams {
     const DWideInst* winst;
     int32_t tw_tlas_nodes;
     float tw_wscale;                 // the local rays' widening factor (option wide_delta_scale / 1000)
+    // tile order (render.hip TileOrder; option tile_order): block -> tile of the megakernels, or
+    // null = row-major XCD groups (device.h xcd_tile); tile_cost: per tile {start, end} of its
+    // wave (s_memrealtime), recorded by the first render of a camera and chunk selection
+    const uint32_t* tile_order;
+    unsigned long long* tile_cost;
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters
-// Compacted bounce render: words [32, 64) of the counters.  Level k (1..kMaxQueueLevels): its ray
-// count at kQueueCount + k and its number of tiles with rays at kQueueTiles + k (k_qscan);
-// k_queue_reset zeroes them (and the tile masks) after the last level.
-constexpr int kQueueCount = 32, kQueueTiles = 48;
+// Compacted bounce render arena header (u64 words at RenderParams::qhdr): [L] the first record of
+// level L (1..kMaxQueueLevels), [kQHdrCap + L] the records per region of level L, and from word
+// kQHdrCnt the (level, region) counters, 128 B apart; k_queue_done zeroes the counters after
+// the last level.
 constexpr int kMaxQueueLevels = 15;
+constexpr int kQRegions = 32;
+constexpr int kQHdrCap = 16, kQHdrCnt = 64, kQCntStride = 16;
+constexpr int kQHdrWords = kQHdrCnt + kMaxQueueLevels * kQRegions * kQCntStride;
 constexpr int kCounterShadowTraced = 13;
 constexpr int kCounterTies = 26;     // wide walks re-walked in reference order (equal-t candidates, wide.h)
 constexpr int kMaxDepthGPU = 16;     // trace() levels kept in private memory per lane (deeper: RenderParams::deep)

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -177,26 +178,59 @@ __device__ __forceinline__ void point_lights(const RenderParams& P, const DMater
 // ---- compacted bounce render (mirror/conductor scenes, one traced sample per pixel) --------
 // The primary pass renders every pixel's primary ray and shadow rays in the spill-free
 // primary instantiation; a lane whose hit is a mirror or conductor below maxRecursionDepth
-// writes its reflected ray to its pixel's level-1 record instead of tracing it, and the wave
-// stores the ballot of those lanes as its tile mask.  Per level, k_qscan lists the tiles with
-// rays and prefixes their counts, and k_bounce traces the level's rays in batches of 64
-// consecutive rays in tile order (a batch holds neighbouring pixels' rays: coherent walks),
-// writing the next level the same way.  A ray that ends resolves its sample backward through
-// its pixel's records with the per-level NaN guard, Lo_k + M_k * L_(k+1)
-// (Object+Extension.swift:189-206, 252-283), and stores the pixel: the operations of the
-// recursion on the same values, so frames are identical.  No same-address atomics: returning
-// atomics on one counter from thousands of waves serialize (~85 ns each, measured).
+// writes its reflected ray to a level-1 record instead of tracing it.  Records are compacted per
+// level: a wave reserves consecutive records for its reflecting lanes with ONE atomic on one of
+// kQRegions counters (q_reserve; region = the wave's block mod kQRegions, so no counter is hit
+// by more than 1/32 of the waves: returning atomics on one address serialize, ~85 ns each,
+// measured), so a level holds only its rays (C5's scratch was 16 slots x 4
+// levels x one 128-B record per pixel = 68 GB).  Per level, k_bounce traces the level's rays in
+// batches of 64 consecutive records (one tile's reflecting pixels are consecutive: coherent
+// walks) and reserves the next level the same way, each record keeping its parent's index.  A
+// ray that ends resolves its sample backward along the parents with the per-level NaN guard,
+// Lo_k + M_k * L_(k+1) (Object+Extension.swift:189-206, 252-283), and stores the pixel: the
+// operations of the recursion on the same values, so frames are identical.  A region that
+// overflows its capacity drops the records (k_queue_done reports each level's largest region
+// count; the host grows the arena and renders that frame again, render.hip wait_impl).
+
+__device__ __forceinline__ unsigned long long* q_counter(const RenderParams& P, int level, int region) {
+    return P.qhdr + kQHdrCnt + ((size_t)(level - 1) * kQRegions + (size_t)region) * kQCntStride;
+}
+// Wave-level reservation of level `level` records in `region`: the active lanes of `m` (the ballot
+// of `want`) get consecutive records with ONE atomic.  q_issue sends it (the first active lane
+// holds the old count); the caller forms the records meanwhile and q_index reads the result:
+// the lane's record, or -1 (no want, or the region is full: the frame is rendered again with a
+// larger arena).
+struct QTicket { unsigned long long base; int first; };
+__device__ __forceinline__ QTicket q_issue(const RenderParams& P, int level, int region, unsigned long long m) {
+    QTicket t;
+    t.first = __builtin_ctzll(__ballot(1));
+    t.base = 0;
+    if ((int)(threadIdx.x & 63) == t.first) t.base = atomicAdd(q_counter(P, level, region), (unsigned long long)__popcll(m));
+    return t;
+}
+__device__ __forceinline__ long long q_index(const RenderParams& P, int level, int region, unsigned long long m,
+                                             bool want, const QTicket& t) {
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)t.base, t.first);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(t.base >> 32), t.first);
+    const unsigned long long idx =
+        ((unsigned long long)lo | ((unsigned long long)hi << 32)) + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+    const unsigned long long cap = P.qhdr[kQHdrCap + level];
+    if (!want || idx >= cap) return -1;
+    return (long long)(P.qhdr[level] + (unsigned long long)region * cap + idx);
+}
 
 // The reflected ray of a mirror/conductor hit and its multiplier (Object+Extension.swift:
-// 189-206, 252-275) into record q; the parent's Lo follows after its shadow walks.
-__device__ __forceinline__ void queue_write(const RenderParams& P, long long q, const DMaterial& M, const V3& d,
-                                            const V3& N, const V3& p, PCG32& rng, double time, int i, int j) {
-    V3 mult;
+// 189-206, 252-275): the record's ray; the parent's Lo follows after its shadow walks.
+struct QRay { V3 o, d, mult; unsigned long long rng; };
+__device__ __forceinline__ QRay queue_ray(const RenderParams& P, const DMaterial& M, const V3& d, const V3& N,
+                                          const V3& p, PCG32& rng) {
+    QRay r;
     if (M.type == RT_MAT_MIRROR) {
-        mult = ld3(M.mirror);
+        r.mult = ld3(M.mirror);
     } else {
         const double cosI = smax(0.0, -dot(d, N));
-        mult = fresnel_conductor(M.ior, M.absorption_index, cosI) * ld3(M.mirror);
+        r.mult = fresnel_conductor(M.ior, M.absorption_index, cosI) * ld3(M.mirror);
     }
     V3 rd = normalize(reflect(d, N));
     if (M.roughness != 0.0) {
@@ -207,14 +241,21 @@ __device__ __forceinline__ void queue_write(const RenderParams& P, long long q, 
         rd = (rd + (M.roughness * r1) * b) + (M.roughness * r2) * t;
         rd = normalize(rd);
     }
-    const V3 o = p + N * P.shadow_eps;
+    r.d = rd;
+    r.o = p + N * P.shadow_eps;
+    r.rng = rng.state;
+    return r;
+}
+__device__ __forceinline__ void queue_store(const RenderParams& P, long long q, const QRay& r, double time, int i,
+                                            int j, long long parent) {
     BounceRec& R = P.bounce[q];
-    R.o[0] = o.x; R.o[1] = o.y; R.o[2] = o.z;
-    R.d[0] = rd.x; R.d[1] = rd.y; R.d[2] = rd.z;
-    R.M[0] = mult.x; R.M[1] = mult.y; R.M[2] = mult.z;
-    R.rng = rng.state;
+    R.o[0] = r.o.x; R.o[1] = r.o.y; R.o[2] = r.o.z;
+    R.d[0] = r.d.x; R.d[1] = r.d.y; R.d[2] = r.d.z;
+    R.M[0] = r.mult.x; R.M[1] = r.mult.y; R.M[2] = r.mult.z;
+    R.rng = r.rng;
     R.time = time;
     R.i = i; R.j = j;
+    R.parent = (int32_t)parent;
 }
 __device__ __forceinline__ void queue_write_lo(const RenderParams& P, long long q, const V3& Lo) {
     BounceRec& R = P.bounce[q];
@@ -284,9 +325,10 @@ typedef TwParked TwPark;
 // `park_rng`: the PCG32 state waits in this lane's LDS pixel slot 3 while the rays are traced
 // (BOUNCE) instead of being live - spilled - across the walks
 // QUEUE (primary pass of the compacted bounce render, !BOUNCE): a mirror/conductor hit writes
-// its reflected ray to its pixel's level-1 record (slot `qtile * 64 + lane`, qtile = this wave's
-// tile) and sets `deferred`; k_bounce delivers that pixel.  The PCG32 state is read from
-// pixel slot 3 (the caller parks it there) and (i0, j0) + the lane give its stream.
+// its reflected ray to a level-1 record (q_reserve, region `qregion`) and sets `deferred`;
+// k_bounce delivers that pixel.  The record index waits in pixel slot 0 (the sample sum, written
+// only after trace_path) across the shadow walks.  The PCG32 state is read from pixel slot 3
+// (the caller parks it there) and (i0, j0) + the lane give its stream.
 // The bounce megakernel (C5's mirror scenes) walks the four-wide tree too, at 4 waves/SIMD
 // (MYRT_BOUNCE_WPE): C5 5020 vs 4733 Mrays/s for the binary walk at 6 waves, which was the binary
 // walk's best occupancy; the wide walk at 5 waves spills (4142), DESIGN.md §4.
@@ -296,7 +338,7 @@ typedef TwParked TwPark;
 template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
                          Counts& c, bool park_rng, int i0 = 0, int j0 = 0,
-                         bool* deferred = nullptr, int qtile = 0) {
+                         bool* deferred = nullptr, int qregion = 0) {
     static_assert(!(QUEUE && BOUNCE), "the queued primary pass has no bounce loop");
     auto park = [&]() { if (BOUNCE && park_rng) *pix_slot(3) = __builtin_bit_cast(double, rng.state); };
     auto unpark = [&]() {
@@ -340,20 +382,23 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
             const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && P.max_depth > 0;
             const unsigned long long m = __ballot(want);
             if (m) {
-                // first active lane stores the mask and counts the wave's bounce rays: neither the
-                // lane id nor a per-lane counter stays live across the shadow walks
-                if (pix_lane() == __builtin_ctzll(__ballot(1))) {
-                    P.bmask[qtile] = m;
-                    atomicAdd(&P.counters[1], (unsigned long long)__builtin_popcountll(m));
-                }
+                // the wave's records with one atomic, formed while it returns (the secondary-ray
+                // count is k_queue_done's)
+                const QTicket tk = q_issue(P, 1, qregion, m);
+                QRay qr{};
+                int i = 0, j = 0;
                 if (want) {
                     const int l = pix_lane();                     // the lane's pixel, recomputed
-                    const int i = i0 + l % kTileW, j = j0 + l / kTileW;
-                    const long long q = (long long)qtile * 64 + l;
-                    queued = true;
+                    i = i0 + l % kTileW; j = j0 + l / kTileW;
                     PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*pix_slot(3)),
                                             pixel_seed(i, j));
-                    queue_write(P, q, M, d, N, p, r, time, i, j);
+                    qr = queue_ray(P, M, d, N, p, r);
+                }
+                const long long q = q_index(P, 1, qregion, m, want, tk);
+                if (want) {
+                    queued = true;
+                    *pix_slot(0) = __builtin_bit_cast(double, q);  // not live across the shadow walks
+                    if (q >= 0) queue_store(P, q, qr, time, i, j, -1);
                 }
             }
         }
@@ -366,7 +411,9 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
             point_lights<COUNT, WALK, !BOUNCE || MYRT_BOUNCE_WIDE, TwPark>(P, M, N, p, d, time, st, c, Lo, park, unpark,
                                                                           !QUEUE);
         if (QUEUE && queued) {
-            queue_write_lo(P, (long long)qtile * 64 + pix_lane(), Lo);
+            asm volatile("" ::: "memory");
+            const long long q = __builtin_bit_cast(long long, (double)*pix_slot(0));
+            if (q >= 0) queue_write_lo(P, q, Lo);
             *deferred = true;
             L = v3(0, 0, 0);
             break;
@@ -452,7 +499,9 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
     // recomputed from a fresh lane id where it is needed after the walks (pix_lane), not kept
     // live - spilled - across them.
     const int gx = (P.cam.width + kTileW - 1) / kTileW;
-    const int tile = xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
+    const int tile = P.tile_order ? (int)P.tile_order[blockIdx.x] : xcd_tile((int)blockIdx.x, (int)gridDim.x, P.xcd_remap);
+    // tile order measurement (option tile_order): the wave's start and end by block
+    if (P.tile_cost && pix_lane() == 0) P.tile_cost[2 * (size_t)blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const int chunk = P.chunk_first + (tile / gx) * P.chunk_step;     // slot = tile / gx
     // the tile's corner in VGPRs: the kernel's SGPRs are at the 106 limit, and uniform values
     // live across the walks there are spilled to VGPR lanes and restored with v_readlane
@@ -531,7 +580,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             // across the walks; the memory clobber makes the reloads real loads.
             if (!BOUNCE) *pix_slot(3) = __builtin_bit_cast(double, rng.state);
             const V3 col = trace_path<COUNT, BOUNCE, WALK, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt, true,
-                                                                 i0, j0, &deferred, tile);
+                                                                 i0, j0, &deferred, (int)(blockIdx.x % kQRegions));
             asm volatile("" ::: "memory");
             if (!BOUNCE) {
                 const int l2 = pix_lane();
@@ -571,6 +620,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
         }
     }
 #endif
+    if (P.tile_cost && lane == 0) P.tile_cost[2 * (size_t)blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     // ray / work counters: one atomic per wave
     const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
                              s2 = wave_sum(cnt.shadow_traced), s3 = wave_sum(cnt.ties);
@@ -618,100 +668,27 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
 
 namespace myrt {
 namespace dev {
-// Per level: the tiles with rays at `level` (their mask is non-zero) and the exclusive prefix of
-// their ray counts, in tile order; totals to the counters.  Two passes over blocks of
-// kQScanTiles tiles (4 consecutive tiles per thread, coalesced): k_qcount writes each block's
-// (rays, tiles) totals, k_qscan prefixes them and writes the list.  (One 1024-thread block
-// walking the whole mask took ~250 us per level on C5.)
-constexpr int kQScanThreads = 256, kQScanTiles = 4 * kQScanThreads;
-__device__ __forceinline__ unsigned long long* qscan_blocks(const RenderParams& P) {
-    return reinterpret_cast<unsigned long long*>(P.bact + 2 * (size_t)P.bounce_tiles);
-}
-// this thread's 4 tiles: per-tile ray counts, packed (rays | tiles << 32) total
-__device__ __forceinline__ unsigned long long qscan_tiles(const RenderParams& P, int level, int base, unsigned c[4]) {
-    const int n = P.bounce_tiles;
-    const unsigned long long* m = P.bmask + (size_t)(level - 1) * n;
-    unsigned long long tot = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        c[k] = base + k < n ? (unsigned)__popcll(m[base + k]) : 0u;
-        tot += (unsigned long long)c[k] | (c[k] ? (1ull << 32) : 0ull);
-    }
-    return tot;
-}
+// Block sum of one u64 per thread over kSumThreads threads (the node-list passes below).
+constexpr int kSumThreads = 256;
 __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long x, unsigned long long* s_w) {
     x = wave_sum(x);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = x;
     __syncthreads();
     unsigned long long t = 0;
 #pragma unroll
-    for (int w = 0; w < kQScanThreads / 64; ++w) t += s_w[w];
+    for (int w = 0; w < kSumThreads / 64; ++w) t += s_w[w];
     __syncthreads();
     return t;
 }
-__global__ __launch_bounds__(kQScanThreads) void k_qcount(RenderParams P, int level) {
-    __shared__ unsigned long long s_w[kQScanThreads / 64];
-    unsigned c[4];
-    const unsigned long long tot =
-        block_sum_u64(qscan_tiles(P, level, blockIdx.x * kQScanTiles + threadIdx.x * 4, c), s_w);
-    if (threadIdx.x == 0) qscan_blocks(P)[blockIdx.x] = tot;
-}
-__global__ __launch_bounds__(kQScanThreads) void k_qscan(RenderParams P, int level) {
-    __shared__ unsigned long long s_w[kQScanThreads / 64];
-    const int t = threadIdx.x, lane = t & 63, n = P.bounce_tiles;
-    const unsigned long long* blk = qscan_blocks(P);
-    unsigned long long before = 0;                       // the blocks before this one
-    for (int k = t; k < (int)blockIdx.x; k += kQScanThreads) before += blk[k];
-    before = block_sum_u64(before, s_w);
-    unsigned c[4];
-    const int base = blockIdx.x * kQScanTiles + t * 4;
-    const unsigned long long mine = qscan_tiles(P, level, base, c);
-    unsigned long long inc = mine;                       // inclusive scan over the wave, then the block
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const unsigned long long y = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += y;
-    }
-    if (lane == 63) s_w[t >> 6] = inc;
-    __syncthreads();
-    unsigned long long ex = before + inc - mine;
-    for (int w = 0; w < (t >> 6); ++w) ex += s_w[w];
-    unsigned run = (unsigned)ex, at = (unsigned)(ex >> 32);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (c[k]) {
-            P.bact[at] = (uint32_t)(base + k);
-            P.bact[n + at] = run;
-            ++at;
-            run += c[k];
-        }
-    }
-    if (blockIdx.x == gridDim.x - 1 && t == kQScanThreads - 1) {
-        P.counters[kQueueCount + level] = run;
-        P.counters[kQueueTiles + level] = at;
-    }
-}
-
-// Position of the r-th set bit (r < popcount(m)).
-__device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned r) {
-    int pos = 0;
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        const unsigned lo = (unsigned)__popcll(m & ((1ull << w) - 1ull));
-        if (r >= lo) { r -= lo; m >>= w; pos += w; }
-    }
-    return pos;
-}
-__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long x, int src) {
-    const unsigned lo = (unsigned)__shfl((int)(unsigned)x, src, 64), hi = (unsigned)__shfl((int)(unsigned)(x >> 32), src, 64);
-    return (unsigned long long)lo | ((unsigned long long)hi << 32);
-}
 
 // One level of the compacted bounce render: the rays trace(depth = level), one lane per ray;
-// wave w of the grid takes the batches of 64 consecutive rays (tile order) w, w + G, ...
-// A mirror/conductor hit below maxRecursionDepth writes its pixel's level + 1 record (its own
-// Lo follows after the shadow walks) and sets its bit in the tile's next-level mask; any other
-// end resolves the sample backward through its pixel's records and stores the pixel.
+// wave w of the grid takes the batches of 64 consecutive records w, w + G, ... of the level's
+// regions laid end to end (lane r < kQRegions holds region r's count, clamped to the capacity,
+// and the exclusive prefix).  A mirror/conductor hit below maxRecursionDepth reserves a
+// level + 1 record (q_reserve, region = the batch number mod kQRegions: a region takes at most
+// ceil(batches / kQRegions) batches), writes its reflected ray there with this record as the
+// parent, and its own Lo after the shadow walks; any other end resolves the sample backward
+// along the parents and stores the pixel.
 #ifndef MYRT_QUEUE_WPE
 #define MYRT_QUEUE_WPE 4
 #endif
@@ -721,114 +698,112 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
     extern __shared__ unsigned long long lds_stack[];
     const int lane = threadIdx.x & 63;
     Counts cnt{};
-    const unsigned T = (unsigned)P.counters[kQueueCount + level];     // written by k_qscan (previous launch)
-    const unsigned A = (unsigned)P.counters[kQueueTiles + level];
-    const int ntiles = P.bounce_tiles;
-    const uint32_t* atile = P.bact;
-    const uint32_t* apre = P.bact + ntiles;
-    const unsigned long long* mask = P.bmask + (size_t)(level - 1) * ntiles;
+    const unsigned long long cap = P.qhdr[kQHdrCap + level], lbase = P.qhdr[level];
+    const unsigned long long cr = lane < kQRegions ? *q_counter(P, level, lane) : 0ull;   // k_bounce(level - 1) / primary pass
+    const unsigned c = (unsigned)(cr < cap ? cr : cap);
+    unsigned inc = c;                                    // inclusive prefix over the regions
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned y = (unsigned)__shfl_up((int)inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    const unsigned ex = inc - c;
+    const unsigned T = (unsigned)__shfl((int)inc, 63, 64);
     MYRT_STACK(st, lds_stack);
     st.uni_spill = true;
     for (unsigned x0 = blockIdx.x * 64u; x0 < T; x0 += gridDim.x * 64u) {
-        // the batch's first tile: the last active tile whose prefix is <= x0 (64-way search)
-        unsigned lo = 0, hi = A;                        // apre[lo] <= x0 < apre[hi] (apre[A] = T)
-        while (hi - lo > 1) {
-            const unsigned pos = lo + (unsigned)(((unsigned long long)(hi - lo) * (unsigned)lane) >> 6);
-            const unsigned long long le = __ballot(apre[pos] <= x0);
-            const int last = 63 - __builtin_clzll(le);
-            const unsigned nlo = (unsigned)__builtin_amdgcn_readlane((int)pos, last);
-            hi = last < 63 ? (unsigned)__builtin_amdgcn_readlane((int)pos, last + 1) : hi;
-            lo = nlo;
-        }
-        // the batch spans at most 64 active tiles from there: lane l holds tile lo + l
-        const unsigned a = lo + (unsigned)lane;
-        const bool in = a < A;
-        const unsigned pre = in ? apre[a] : 0xffffffffu;
-        const unsigned tl = in ? atile[a] : 0u;
-        const unsigned long long mk = in ? mask[tl] : 0ull;
         const unsigned b = x0 + (unsigned)lane;          // this lane's ray
-        int jl = 0, jh = 64;                             // its tile: the last lane with pre <= b
+        int jl = 0, jh = kQRegions;                      // its region: the last one with ex <= b
 #pragma unroll
-        for (int s = 0; s < 6; ++s) {
+        for (int s = 0; s < 5; ++s) {
             const int mid = (jl + jh) >> 1;
-            if ((unsigned)__shfl((int)pre, mid, 64) <= b) jl = mid; else jh = mid;
+            if ((unsigned)__shfl((int)ex, mid, 64) <= b) jl = mid; else jh = mid;
         }
-        const unsigned rank = b - (unsigned)__shfl((int)pre, jl, 64);
-        const unsigned long long myMask = shfl_u64(mk, jl);
-        const unsigned myTile = (unsigned)__shfl((int)tl, jl, 64);
+        const long long g = (long long)(lbase + (unsigned long long)jl * cap +
+                                        (unsigned long long)(b - (unsigned)__shfl((int)ex, jl, 64)));
         if (b >= T) continue;
-        const int bit = nth_set_bit(myMask, rank);
-        const long long slot = (long long)myTile * 64 + bit;
-        const long long g = (long long)(level - 1) * P.bounce_cap + slot;
         const BounceRec& R = P.bounce[g];
         const V3 o = ld3(R.o), d = ld3(R.d);
         const double time = WALK == kWalkIdentity ? 0.0 : R.time;
-        V3 L;
-        bool ends = true;
-        if (!P.has_tlas) {
-            L = v3(0, 0, 0);
-        } else {
+        V3 L = v3(0, 0, 0);
+        bool hit = false, want = false, computeDirect = false;
+        V3 p, N, Lo;
+        const DMaterial* Mp = nullptr;
+        if (P.has_tlas) {
             const V3 inv = rcp(d);
             Hit h;
             walk_closest<false, WALK>(P, o, d, inv, 0.0, time, h, st, cnt);
             if (h.inst < 0) {
                 L = ld3(P.background);
             } else {
-                V3 p, Ngeo;
+                hit = true;
+                V3 Ngeo;
                 hit_geometry<false>(P, o, d, time, h, p, Ngeo, cnt);
                 const DInstance& I = P.insts[h.inst];
-                const DMaterial& M = P.mats[max(0, min(P.num_mats - 1, I.material - 1))];
+                Mp = &P.mats[max(0, min(P.num_mats - 1, I.material - 1))];
                 const bool frontFacing = dot(d, Ngeo) < 0;
-                const V3 N = frontFacing ? Ngeo : -Ngeo;
-                const bool computeDirect = !(M.ior > 0) || frontFacing;
-                V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
-                const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && level < P.max_depth;
-                const long long q = want ? (long long)level * P.bounce_cap + slot : -1ll;
-                if (want) {
-                    const BounceRec& Rs = P.bounce[g];
-                    PCG32 r = PCG32::resume(Rs.rng, pixel_seed(Rs.i, Rs.j));
-                    queue_write(P, q, M, d, N, p, r, Rs.time, Rs.i, Rs.j);
-                    atomicOr(&P.bmask[(size_t)level * ntiles + myTile], 1ull << bit);
-                    cnt.secondary++;
-                }
-                auto none = []() {};
-                if (computeDirect) point_lights<false, WALK, true>(P, M, N, p, d, time, st, cnt, Lo, none, none);
-                if (want) {
-                    queue_write_lo(P, q, Lo);
-                    ends = false;
-                } else {
-                    L = isfin(Lo) ? Lo : v3(0, 0, 0);
-                }
+                N = frontFacing ? Ngeo : -Ngeo;
+                computeDirect = !(Mp->ior > 0) || frontFacing;
+                Lo = computeDirect ? ld3(P.ambient) * ld3(Mp->ambient) : v3(0, 0, 0);
+                want = (Mp->type == RT_MAT_MIRROR || Mp->type == RT_MAT_CONDUCTOR) && level < P.max_depth;
             }
         }
-        if (ends) {      // back through the pixel's records: Lo_k + M_k * L_(k+1), NaN guard per level
+        const unsigned long long m = __ballot(want);
+        long long q = -1;
+        if (m) {                                         // the records, formed while the atomic returns
+            const int region = (int)((x0 >> 6) % kQRegions);
+            const QTicket tk = q_issue(P, level + 1, region, m);
+            QRay qr{};
+            if (want) {
+                PCG32 r = PCG32::resume(R.rng, pixel_seed(R.i, R.j));
+                qr = queue_ray(P, *Mp, d, N, p, r);
+            }
+            q = q_index(P, level + 1, region, m, want, tk);
+            if (q >= 0) queue_store(P, q, qr, R.time, R.i, R.j, g);
+        }
+        if (hit) {
+            auto none = []() {};
+            if (computeDirect) point_lights<false, WALK, true>(P, *Mp, N, p, d, time, st, cnt, Lo, none, none);
+            if (!want) L = isfin(Lo) ? Lo : v3(0, 0, 0);
+            else if (q >= 0) queue_write_lo(P, q, Lo);
+        }
+        if (!want) {     // back along the parents: Lo_k + M_k * L_(k+1), NaN guard per level
             int pi = 0, pj = 0;
+            long long gg = g;
             for (int lev = level; lev >= 1; --lev) {
-                const BounceRec& Q = P.bounce[(long long)(lev - 1) * P.bounce_cap + slot];
-                const V3 Lo = ld3(Q.Lo) + ld3(Q.M) * L;
-                L = isfin(Lo) ? Lo : v3(0, 0, 0);
+                const BounceRec& Q = P.bounce[gg];
+                const V3 Lq = ld3(Q.Lo) + ld3(Q.M) * L;
+                L = isfin(Lq) ? Lq : v3(0, 0, 0);
                 pi = Q.i; pj = Q.j;
+                gg = Q.parent;
             }
             const V3 pixel = v3(0.0 + L.x, 0.0 + L.y, 0.0 + L.z);   // the sample sum (one sample)
             store_pixel(P, pi, pj, pixel / (double)P.cam.samples);
         }
     }
-    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
-                             s2 = wave_sum(cnt.shadow_traced), s3 = wave_sum(cnt.ties);
+    const unsigned long long s0 = wave_sum(cnt.shadow), s2 = wave_sum(cnt.shadow_traced), s3 = wave_sum(cnt.ties);
     if (lane == 0) {
         if (s0) atomicAdd(&P.counters[0], s0);
-        if (s1) atomicAdd(&P.counters[1], s1);
         if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
         if (s3) atomicAdd(&P.counters[kCounterTies], s3);
     }
 }
 
-// After the last level: tile masks and queue words back at zero for the next launch.
-__global__ void k_queue_reset(RenderParams P, int levels) {
-    const size_t n = (size_t)levels * P.bounce_tiles;
-    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x)
-        P.bmask[k] = 0ull;
-    if (blockIdx.x == 0 && kQueueCount + (int)threadIdx.x < kCounterWords) P.counters[kQueueCount + threadIdx.x] = 0ull;
+// After the last level (one wave): every level's largest region count to the host (qneed: the
+// arena a frame needs), the records reserved over all levels (= the secondary rays) to the
+// counters, and the region counters back at zero for the next launch.
+__global__ void k_queue_done(RenderParams P, int levels) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long tot = 0;
+    for (int L = 1; L <= levels; ++L) {
+        const unsigned long long c = lane < kQRegions ? *q_counter(P, L, lane) : 0ull;
+        tot += c;
+        const unsigned long long mx = wave_max(c);
+        if (lane < kQRegions) *q_counter(P, L, lane) = 0ull;
+        if (lane == 0 && P.qneed) P.qneed[L] = mx;
+    }
+    tot = wave_sum(tot);
+    if (lane == 0 && tot) atomicAdd(&P.counters[1], tot);
 }
 
 // ---- compacted node lists (option node_lists; render_full.h level / shading passes) ----------
@@ -845,7 +820,7 @@ __global__ void k_queue_reset(RenderParams P, int levels) {
 // k_ccount writes each block's count, k_clist prefixes the blocks before its own, writes the list
 // and its length.
 constexpr int kCListThreads = 256, kCListShade = 7;
-static_assert(kCListThreads == kQScanThreads, "block_sum_u64 sums kQScanThreads lanes");
+static_assert(kCListThreads == kSumThreads, "block_sum_u64 sums kSumThreads lanes");
 // the log entries [k_lo, k_hi) the groups of `level` run over (level < 0: the whole log, also
 // k_events' walk-indexed log: tree 0)
 __host__ __device__ inline void clist_span(int tree, int per, int slots, int level, int& k_lo, int& k_hi) {
@@ -1053,10 +1028,22 @@ constexpr int kRenderBatches = 8;   // rt_render: chunk batches per replica (pro
 // on every replica, so consecutive frames overlap on the GPU: the next frame's tiles fill the
 // compute units the previous frame's slowest tiles leave idle (tools/probe_overlap.py).
 constexpr int kInFlight = RT_MAX_IN_FLIGHT;
-// Queued bounce rays of one stream's renders (BounceRec, levels x records per level)
+// Queued bounce rays of one stream's renders (queue_arena): the header (kQHdrWords u64: level
+// bases, capacities, region counters), then the records, level by level, kQRegions regions each.
+// In-flight slots size their arenas by the need measured on earlier frames (by_need: a frame that
+// overflows is rendered again, wait_impl); the replica's and the device path's arenas take the
+// worst case (every pixel reflects), since nothing waits for their renders to check.
 struct BounceArena {
-    void* base = nullptr;                          // records, tile masks, tile list (queue_arena)
-    int64_t levels = 0, tiles = 0;                 // capacity
+    void* base = nullptr;
+    int64_t levels = 0;
+    int64_t cap[kMaxQueueLevels + 1] = {};         // records per region of each level
+    int64_t recs = 0;                              // records behind the header
+    unsigned long long hdr[kQHdrCnt] = {};         // host image of the header's bases and capacities
+    bool by_need = false;
+    unsigned long long* qneed = nullptr;           // host-mapped (by_need): k_queue_done's need per level
+    unsigned long long* qneed_dev = nullptr;
+    bool check = false;                            // a render on this arena reported qneed, unchecked
+    int64_t check_levels = 0;
 };
 // Compacted bounce render: device bytes one launch may take for its queues (else the megakernel)
 constexpr int64_t kQueueBytesCap = 16ll << 30;
@@ -1101,8 +1088,33 @@ struct Flight {
     bool counters_zero = false;
     bool counters_valid = false;                   // host_counters hold this render's counts (k_counters_out ran)
     bool used = false;                             // this replica took part in the render
+    std::function<int32_t()> relaunch;             // this replica's launches of the slot's render, again
     BounceArena arena;                             // compacted bounce render queues of this slot
     FullScratch full;                              // full trace() passes of the renders on this slot's stream
+};
+
+// ---- tile order (render option tile_order): the longest tiles dispatched first ------------------
+// A frame lasts as long as its slowest tiles: a wave whose lanes walk ~300 steps
+// (grazing rays over the terrain) takes 0.3-0.5 ms alone against 0.07 ms for the median tile, and
+// in row-major order some of them start late and form the frame's tail - the tail of the last
+// frame of a pipelined run, and the whole latency of a strong split's share.  The first render of
+// a (camera, chunk selection) records every wave's start and end (RenderParams::tile_cost); the
+// next renders of it dispatch the slowest XCD tile groups first (longest-processing-time order),
+// the rest in row-major order behind them.  Which wave renders a pixel does not change the pixel
+// (each pixel seeds its own PCG32, Object+Extension.swift:294), so frames are identical.
+struct TileOrderKey {
+    double eye[3], w[3];
+    int32_t width, height, first, step, chunks, group;
+    bool operator==(const TileOrderKey& o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
+};
+struct TileOrder {
+    TileOrderKey key{};
+    int state = 0;                            // 1: costs being measured (ev), 2: order ready
+    int64_t n = 0;                            // tiles (blocks of the launch)
+    uint32_t* order = nullptr;                // block -> tile
+    unsigned long long* cost = nullptr;       // per tile {start, end} (s_memrealtime)
+    hipEvent_t ev = nullptr;
+    int64_t used = 0;                         // last use (eviction)
 };
 
 struct DeviceReplica {
@@ -1123,7 +1135,8 @@ struct DeviceReplica {
     double* jitter = nullptr;
     FullScratch full;                         // full trace() passes on the replica stream
     void* deep = nullptr; int64_t deep_cap = 0;   // deep trace() frames (render_full<.., true>)
-    std::vector<void*> retired;               // grown scratch's predecessors (retire(), freed at destroy)
+    std::vector<void*> retired;               // grown scratch's predecessors (retire(), freed by reclaim())
+    int64_t retired_bytes = 0;
     unsigned long long* counters = nullptr;   // kCounterWords x u64
     unsigned long long* wave_times = nullptr; int64_t wave_times_cap = 0;   // rt_debug_wave_times
     hipStream_t stream = nullptr;
@@ -1141,12 +1154,15 @@ struct DeviceReplica {
     int64_t bytes = 0;
     int cus = 256;                            // compute units (k_bounce grid)
     BounceArena arena;                        // compacted bounce queues of the replica stream
+    int64_t qhint[kMaxQueueLevels + 1] = {};  // largest region count seen per level (by_need arenas)
     // rt_render_device / rt_render_device_counted (the caller's stream): counters, pass scratch and
     // queues of their own, so device renders may overlap the replica-stream and slot renders
     unsigned long long* dev_counters = nullptr;
     FullScratch dev_full;
     BounceArena dev_arena;
     Flight fl[kInFlight];                     // rt_render_submit slots
+    std::vector<TileOrder> orders;            // tile orders by camera and chunk selection (option tile_order)
+    int64_t order_clock = 0;
 };
 
 }  // namespace
@@ -1158,9 +1174,11 @@ enum OptId {
     kOptWide, kOptUnified, kOptUnifiedTransformed, kOptCompactRecords, kOptCompactTris, kOptXcdGroup,
     kOptQueue, kOptQueueLevels, kOptHitlog, kOptNodeshade, kOptLevels, kOptTreePpw, kOptFullFlights,
     kOptDeepCapMb, kOptBatches, kOptZerocopy, kOptSubmitEvents, kOptSubmitCounters, kOptSubmitDma,
-    kOptDebugFailReplica, kOptWideDeltaScale, kOptNodeLists, kOptCount
+    kOptDebugFailReplica, kOptWideDeltaScale, kOptNodeLists, kOptTileOrder, kOptCount
 };
-struct OptDef { const char* name; int64_t def, lo, hi; };
+// `unsafe` options are test hooks: rt_scene_set_option refuses them (RT_ERR_INVALID_ARG); only the
+// non-production entry point rt_scene_set_unsafe_option sets them (rtcore.h).
+struct OptDef { const char* name; int64_t def, lo, hi; bool unsafe = false; };
 static const OptDef kOptDefs[kOptCount] = {
     {"wide", 1, 0, 1},                    // conservative FP32 four-wide walk on identity scenes (wide.h)
     {"unified", 1, 0, 1},                 // one-stack TLAS+BLAS walks (0: the nested general walk)
@@ -1168,7 +1186,7 @@ static const OptDef kOptDefs[kOptCount] = {
     {"compact_records", 1, 0, 1},         // float32-bound BLAS records when exact (layout.h CRec)
     {"compact_tris", 1, 0, 1},            // float32-vertex triangles when exact (layout.h CTri)
     {"xcd_group", 0, 0, 64},              // tiles per XCD run (device.h xcd_tile); 0 = max(2, width / 960)
-    {"queue", 1, 0, 1},                   // compacted bounce render for mirror scenes (k_qscan / k_bounce)
+    {"queue", 1, 0, 1},                   // compacted bounce render for mirror scenes (k_bounce per level)
     {"queue_levels", -1, -1, 15},         // timing probe: bounce levels of the compacted render (-1 = all)
     {"hitlog", -1, -1, 64},               // closest hits logged per pixel for render_full (-1 = sized automatically)
     {"nodeshade", 1, 0, 1},               // node-parallel shading of logged hits (render_full.h k_shade)
@@ -1181,11 +1199,12 @@ static const OptDef kOptDefs[kOptCount] = {
     {"submit_events", 1, 0, 1},           // kernel-timing events on renders that ask for them
     {"submit_counters", 1, 0, 1},         // ray counters delivered per submitted render
     {"submit_dma", 0, 0, 2},              // submitted delivery: 0 kernel stores, 1 staging + DMA, 2 staging only
-    {"debug_fail_replica", -1, -1, 1 << 20},   // test hook: launch failure injected on this replica
-    {"wide_delta_scale", 1000, 0, 1000000},    // test hook: the four-wide walk's widening (wdelta) in
-                                               // 1/1000 of the exact bound; < 1000 voids wide.h's
-                                               // exactness proof (tests show that it has teeth)
+    {"debug_fail_replica", -1, -1, 1 << 20, true},   // test hook: launch failure injected on this replica
+    {"wide_delta_scale", 1000, 0, 1000000, true},    // test hook: the four-wide walk's widening (wdelta)
+                                                     // in 1/1000 of the exact bound; < 1000 voids wide.h's
+                                                     // exactness proof (tests show that it has teeth)
     {"node_lists", 1, 0, 1},              // level passes past 0 and node shading over compacted node lists
+    {"tile_order", 0, 0, 100},            // % of XCD tile groups dispatched first, slowest first (TileOrder; 0 = row-major)
 };
 
 struct rt_scene {
@@ -1209,16 +1228,18 @@ struct rt_scene {
 
 static int64_t full_scratch_bytes(const FullScratch& f) {
     return f.cap_px * 16 + f.hitlog_cap * (int64_t)sizeof(DHitRec) +
-           f.nodes_cap * (int64_t)(sizeof(DNodeRec) + 3 * sizeof(double)) + f.walks_cap * 4 + f.nflags_cap;
+           f.nodes_cap * (int64_t)(sizeof(DNodeRec) + 3 * sizeof(double)) + f.walks_cap * 4 + f.nflags_cap +
+           f.clist_cap * (int64_t)sizeof(uint32_t);
 }
 static int64_t arena_bytes(const BounceArena& a) {
-    return a.base ? a.levels * a.tiles * 64 * (int64_t)sizeof(BounceRec) + a.levels * a.tiles * 8 + a.tiles * 8 : 0;
+    return a.base ? (int64_t)kQHdrWords * 8 + a.recs * (int64_t)sizeof(BounceRec) : 0;
 }
 // device scratch a replica holds now (rt_scene_info.scratch_bytes): grown on demand, kept for reuse
 static int64_t scratch_bytes(const DeviceReplica& r) {
     int64_t b = full_scratch_bytes(r.full) + full_scratch_bytes(r.dev_full) + arena_bytes(r.arena) +
-                arena_bytes(r.dev_arena) + r.deep_cap + r.out_cap_px * 28 + r.wave_times_cap * 24;
+                arena_bytes(r.dev_arena) + r.deep_cap + r.out_cap_px * 28 + r.wave_times_cap * 24 + r.retired_bytes;
     for (const Flight& f : r.fl) b += full_scratch_bytes(f.full) + arena_bytes(f.arena) + f.stage_px * 28;
+    for (const TileOrder& o : r.orders) b += o.n * (int64_t)(sizeof(uint32_t) + 2 * sizeof(unsigned long long));
     return b;
 }
 
@@ -1234,20 +1255,56 @@ static int32_t upload(const std::vector<T>& v, T** dst, int64_t& bytes) {
 // Scratch grows on demand (a larger chunk selection, a deeper scene), but a grown buffer's
 // predecessor is never freed beside renders in flight: hipFree may wait for the whole device
 // (stalling every in-flight render), and a render still queued on another stream - a caller's
-// stream for rt_render_device, an in-flight slot - may still read it.  It is retired instead and
-// freed with the replica (after a device synchronisation); the new buffer is zeroed, where
-// needed, on the growing render's own stream.  Capacities grow by at least 1.5x, so the retired
-// bytes stay within twice the live scratch.
-static void retire(DeviceReplica& r, void* p) {
-    if (p) r.retired.push_back(p);
+// stream for rt_render_device, an in-flight slot - may still read it.  It is retired instead
+// (rt_scene_info.scratch_bytes counts it) and freed by reclaim() once the scene has no render in
+// flight (after a device synchronisation), or with the replica; the new buffer is zeroed, where
+// needed, on the growing render's own stream.  Every growing buffer takes at least 1.5x its old
+// capacity (grow_buf), so a scene whose selections keep creeping up retires O(log) buffers.
+static void retire(DeviceReplica& r, void* p, int64_t bytes) {
+    if (p) { r.retired.push_back(p); r.retired_bytes += bytes; }
 }
 static int64_t grown(int64_t need, int64_t cap) { return std::max(need, cap + cap / 2); }
-
+// Grow *p to hold `need` elements (capacity `cap`, in elements): the old buffer is retired and the
+// new one takes grown(need, cap) elements, or exactly `need` when that much is not available.
+// Returns false (and leaves *p null, cap 0) when not even `need` fits.
+template <class T>
+static bool grow_buf(DeviceReplica& r, T** p, int64_t& cap, int64_t need, size_t elem = sizeof(T)) {
+    if (need <= cap && *p) return true;
+    const int64_t old = cap;
+    retire(r, *p, old * (int64_t)elem);
+    *p = nullptr; cap = 0;
+    const int64_t want = grown(need, old);
+    if (hipMalloc((void**)p, (size_t)want * elem) == hipSuccess) { cap = want; return true; }
+    (void)hipGetLastError();
+    if (want > need && hipMalloc((void**)p, (size_t)need * elem) == hipSuccess) { cap = need; return true; }
+    (void)hipGetLastError();
+    *p = nullptr;
+    return false;
+}
+static void free_retired(DeviceReplica& r) {
+    for (void* p : r.retired) (void)hipFree(p);
+    r.retired.clear();
+    r.retired_bytes = 0;
+}
+// Free the retired scratch once no submitted render of the scene is in flight (the scene lock is
+// held): a device synchronisation first, so a render still queued on a caller's stream
+// (rt_render_device) has finished with it.  Growth is rare, so is the synchronisation.
+static void reclaim(rt_scene* s) {
+    bool any = false;
+    for (const DeviceReplica& r : s->devs) any = any || !r.retired.empty();
+    if (!any) return;
+    for (const rt_scene::Pending& fp : s->flights)
+        if (fp.pending) return;
+    for (DeviceReplica& r : s->devs) {
+        if (r.retired.empty()) continue;
+        if (hipSetDevice(r.device) == hipSuccess && hipDeviceSynchronize() == hipSuccess) free_retired(r);
+        else (void)hipGetLastError();
+    }
+}
 static void free_replica(DeviceReplica& r) {
     (void)hipSetDevice(r.device);
     (void)hipDeviceSynchronize();
-    for (void* p : r.retired) (void)hipFree(p);
-    r.retired.clear();
+    free_retired(r);
     (void)hipFree(r.wnodes); (void)hipFree(r.lbox); (void)hipFree(r.winst);
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
@@ -1273,6 +1330,7 @@ static void free_replica(DeviceReplica& r) {
         (void)hipFree(f.stage_rgb);
         (void)hipFree(f.stage_rgba);
         (void)hipFree(f.arena.base);
+        if (f.arena.qneed) (void)hipHostFree(f.arena.qneed);
         if (f.host_counters) (void)hipHostFree(f.host_counters);
     }
     if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -1282,6 +1340,10 @@ static void free_replica(DeviceReplica& r) {
     if (r.host_rgba) (void)hipHostFree(r.host_rgba);
     for (auto e : r.batch_done) (void)hipEventDestroy(e);
     for (auto e : r.batch_copied) (void)hipEventDestroy(e);
+    for (TileOrder& o : r.orders) {
+        (void)hipFree(o.order); (void)hipFree(o.cost);
+        if (o.ev) (void)hipEventDestroy(o.ev);
+    }
     r = DeviceReplica();
 }
 
@@ -1369,6 +1431,10 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
         HIP_TRY(hipHostMalloc((void**)&f.host_counters, kCounterWords * sizeof(unsigned long long),
                               hipHostMallocMapped));
         HIP_TRY(hipHostGetDevicePointer((void**)&f.host_counters_dev, f.host_counters, 0));
+        HIP_TRY(hipHostMalloc((void**)&f.arena.qneed, (kMaxQueueLevels + 1) * sizeof(unsigned long long),
+                              hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer((void**)&f.arena.qneed_dev, f.arena.qneed, 0));
+        f.arena.by_need = true;
     }
     // the zeroing above ran on the null stream, which does not order against the non-blocking
     // render streams: finish it before any render can start
@@ -1619,10 +1685,10 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         batch = (int32_t)std::max(1.0, std::min((double)P.num_chunks, std::floor(deep_cap(s) / per_chunk)));
         const int64_t need = (int64_t)(per_chunk * batch);
         if (need > r.deep_cap) {
-            retire(r, r.deep);
-            r.deep = nullptr; r.deep_cap = 0;
-            if (hipMalloc(&r.deep, need) != hipSuccess) return fail(RT_ERR_OOM, "device allocation of deep trace() frames failed");
-            r.deep_cap = need;
+            char* d = static_cast<char*>(r.deep);
+            const bool ok = grow_buf(r, &d, r.deep_cap, need, 1);
+            r.deep = d;
+            if (!ok) return fail(RT_ERR_OOM, "device allocation of deep trace() frames failed");
         }
         P.deep = r.deep;
     }
@@ -1647,7 +1713,7 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         const int64_t px = (int64_t)P.num_chunks * 8 * P.cam.width;
         if (px > fs.cap_px) {
             const int64_t cap = grown(px, fs.cap_px);
-            retire(r, fs.events); retire(r, fs.jstart);
+            retire(r, fs.events, fs.cap_px * 8); retire(r, fs.jstart, fs.cap_px * 8);
             fs.events = nullptr; fs.jstart = nullptr; fs.cap_px = 0;
             if (hipMalloc((void**)&fs.events, cap * sizeof(long long)) != hipSuccess ||
                 hipMalloc((void**)&fs.jstart, cap * sizeof(long long)) != hipSuccess) {
@@ -1665,12 +1731,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         // instead of walking them again (option hitlog = K overrides, 0 = off; counting launches walk)
         const int64_t hl = s->opt[kOptHitlog];
         const int64_t slots = count ? 0 : (hl >= 0 ? hl : hit_slots_for(P, dielectric, px));
-        if (slots > 0 && slots * px > fs.hitlog_cap) {
-            retire(r, fs.hitlog);
-            fs.hitlog = nullptr; fs.hitlog_cap = 0;
-            if (hipMalloc((void**)&fs.hitlog, (size_t)(slots * px) * sizeof(DHitRec)) == hipSuccess) fs.hitlog_cap = slots * px;
-            else (void)hipGetLastError();             // no log: render_full walks every ray
-        }
+        if (slots > 0 && slots * px > fs.hitlog_cap)
+            (void)grow_buf(r, &fs.hitlog, fs.hitlog_cap, slots * px);   // none: render_full walks every ray
         const bool log = slots > 0 && slots * px <= fs.hitlog_cap;
         P.hits = log ? fs.hitlog : nullptr;
         P.hit_slots = log ? (int32_t)slots : 0;
@@ -1680,8 +1742,10 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         // kernels take RenderParams by value.
         bool nodeshade = log && s->opt[kOptNodeshade] != 0;
         if (nodeshade && (slots * px > fs.nodes_cap || px > fs.walks_cap)) {
-            const int64_t recs = std::max(slots * px, fs.nodes_cap), pxs = std::max(px, fs.walks_cap);
-            retire(r, fs.nodes); retire(r, fs.node_lo); retire(r, fs.walks);
+            const int64_t recs = slots * px > fs.nodes_cap ? grown(slots * px, fs.nodes_cap) : fs.nodes_cap;
+            const int64_t pxs = px > fs.walks_cap ? grown(px, fs.walks_cap) : fs.walks_cap;
+            retire(r, fs.nodes, fs.nodes_cap * (int64_t)sizeof(DNodeRec));
+            retire(r, fs.node_lo, fs.nodes_cap * 24); retire(r, fs.walks, fs.walks_cap * 4);
             fs.nodes = nullptr; fs.node_lo = nullptr; fs.walks = nullptr; fs.nodes_cap = fs.walks_cap = 0;
             if (hipMalloc((void**)&fs.nodes, (size_t)recs * sizeof(DNodeRec)) == hipSuccess &&
                 hipMalloc((void**)&fs.node_lo, (size_t)recs * 3 * sizeof(double)) == hipSuccess &&
@@ -1689,8 +1753,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
                 fs.nodes_cap = recs;
                 fs.walks_cap = pxs;
             } else {
-                (void)hipGetLastError();              // render_full shades every hit
-                retire(r, fs.nodes); retire(r, fs.node_lo); retire(r, fs.walks);
+                (void)hipGetLastError();              // render_full shades every hit (never used: safe to free)
+                (void)hipFree(fs.nodes); (void)hipFree(fs.node_lo); (void)hipFree(fs.walks);
                 fs.nodes = nullptr; fs.node_lo = nullptr; fs.walks = nullptr;
             }
         }
@@ -1711,12 +1775,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         // with area lights - over hit flags k_events writes for node shading
         const bool want_lists = nodeshade && s->opt[kOptNodeLists] != 0 && slots * px < (int64_t(1) << 32);
         bool flags_ev = want_lists && !levels && alights;
-        if ((levels || flags_ev) && slots * px > fs.nflags_cap) {
-            retire(r, fs.nflags);
-            fs.nflags = nullptr; fs.nflags_cap = 0;
-            if (hipMalloc((void**)&fs.nflags, (size_t)(slots * px)) == hipSuccess) fs.nflags_cap = slots * px;
-            else (void)hipGetLastError();             // depth-first k_events
-        }
+        if ((levels || flags_ev) && slots * px > fs.nflags_cap)
+            (void)grow_buf(r, &fs.nflags, fs.nflags_cap, slots * px);   // none: depth-first k_events
         levels = levels && slots * px <= fs.nflags_cap && px <= fs.cap_px;
         flags_ev = flags_ev && slots * px <= fs.nflags_cap;
         // compacted node lists: entry indices are u32; list + block counts + lengths
@@ -1724,12 +1784,8 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
         const int64_t cblocks = (cgroups + dev::kCListThreads - 1) / dev::kCListThreads;
         const int64_t cwords = slots * px + cblocks + 8;
         lists = want_lists && (levels || flags_ev);
-        if (lists && cwords > fs.clist_cap) {
-            retire(r, fs.clist);
-            fs.clist = nullptr; fs.clist_cap = 0;
-            if (hipMalloc((void**)&fs.clist, (size_t)cwords * sizeof(uint32_t)) == hipSuccess) fs.clist_cap = cwords;
-            else (void)hipGetLastError();             // the per-tile passes
-        }
+        if (lists && cwords > fs.clist_cap)
+            (void)grow_buf(r, &fs.clist, fs.clist_cap, cwords);          // none: the per-tile passes
         lists = lists && cwords <= fs.clist_cap;
         P.clist = lists ? fs.clist : nullptr;
         P.cblk = lists ? fs.clist + slots * px : nullptr;
@@ -1819,51 +1875,179 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
 }
 
 // Compacted bounce render for this launch (render.hip k_bounce): mirror/conductor scenes whose
-// pixels trace one sample (Int(sqrt(spp)) == 1) with maxRecursionDepth <= kMaxQueueLevels;
-// `arena` grows to levels x (tiles x 64) records, the tile masks and k_qscan's tile list
-// (false: allocation refused or failed -> the bounce megakernel).
+// pixels trace one sample (Int(sqrt(spp)) == 1) with maxRecursionDepth <= kMaxQueueLevels.  A
+// region of level L takes at most ceil(tiles / kQRegions) * 64 records (the worst case: every
+// pixel reflects; render.hip q_reserve); by_need arenas take 1.25x the largest region count seen
+// (DeviceReplica::qhint; 1/16 of the worst case before any is known) and grow when that rises.
+// (false: allocation refused or failed -> the bounce megakernel.)
 static bool queue_arena(const rt_scene* s, DeviceReplica& r, BounceArena* arena, RenderParams& P, int64_t tiles,
                         hipStream_t stream) {
     if (!arena || s->opt[kOptQueue] == 0) return false;
     if (P.cam.n != 1 || P.max_depth < 1 || P.max_depth > kMaxQueueLevels) return false;
     const int64_t levels = P.max_depth;
-    // sections at offsets fixed by the allocation's capacity: the tile masks stay where the
-    // previous launch (whatever its size) zeroed them
-    auto bytes = [](int64_t lv, int64_t tl) {
-        return (size_t)(lv * tl * 64) * sizeof(BounceRec) + (size_t)(lv * tl) * sizeof(unsigned long long) +
-               (size_t)(2 * tl) * sizeof(uint32_t) +
-               (size_t)((tl + dev::kQScanTiles - 1) / dev::kQScanTiles) * sizeof(unsigned long long);
-    };
-    if (levels > arena->levels || tiles > arena->tiles) {
+    const int64_t worst = (tiles + kQRegions - 1) / kQRegions * 64;
+    int64_t want[kMaxQueueLevels + 1] = {};
+    bool grow = arena->base == nullptr || levels > arena->levels;
+    for (int64_t L = 1; L <= levels; ++L) {
+        const int64_t h = r.qhint[L];
+        want[L] = !arena->by_need ? worst : std::min(worst, h > 0 ? h + h / 4 + 64 : worst / 16 + 64);
+        grow = grow || arena->cap[L] < want[L];
+    }
+    if (grow) {
         const int64_t lv = std::max(levels, arena->levels);
-        int64_t tl = tiles > arena->tiles ? grown(tiles, arena->tiles) : arena->tiles;
-        if ((int64_t)bytes(lv, tl) > kQueueBytesCap) tl = std::max(tiles, arena->tiles);
-        if ((int64_t)bytes(lv, tl) > kQueueBytesCap) return false;
-        retire(r, arena->base);
+        int64_t cap[kMaxQueueLevels + 1] = {};
+        int64_t recs = 0;
+        for (int64_t L = 1; L <= lv; ++L) {
+            cap[L] = std::max(L <= levels ? want[L] : 0, L <= arena->levels ? arena->cap[L] : 0);
+            recs += kQRegions * cap[L];
+        }
+        const size_t bytes = (size_t)kQHdrWords * 8 + (size_t)recs * sizeof(BounceRec);
+        if ((int64_t)bytes > kQueueBytesCap) return false;
+        retire(r, arena->base, arena_bytes(*arena));
         arena->base = nullptr;
-        arena->levels = arena->tiles = 0;
-        // zeroed on the render's own stream: a plain hipMemset runs on the null stream, which does
-        // not order against the library's non-blocking streams - it could zero the masks and
-        // records while this render's kernels already use them (undelivered mirror pixels)
-        if (hipMalloc(&arena->base, bytes(lv, tl)) != hipSuccess ||
-            hipMemsetAsync(arena->base, 0, bytes(lv, tl), stream) != hipSuccess) {
+        arena->levels = 0;
+        arena->recs = 0;
+        std::memset(arena->hdr, 0, sizeof(arena->hdr));
+        int64_t at = 0;
+        for (int64_t L = 1; L <= lv; ++L) {
+            arena->hdr[L] = (unsigned long long)at;
+            arena->hdr[kQHdrCap + L] = (unsigned long long)cap[L];
+            at += kQRegions * cap[L];
+        }
+        // header written and counters zeroed on the render's own stream: a plain hipMemset runs on
+        // the null stream, which does not order against the library's non-blocking streams
+        if (hipMalloc(&arena->base, bytes) != hipSuccess ||
+            hipMemsetAsync(arena->base, 0, (size_t)kQHdrWords * 8, stream) != hipSuccess ||
+            hipMemcpyAsync(arena->base, arena->hdr, sizeof(arena->hdr), hipMemcpyHostToDevice, stream) != hipSuccess) {
             (void)hipGetLastError();
             (void)hipFree(arena->base);
             arena->base = nullptr;
             return false;
         }
         arena->levels = lv;
-        arena->tiles = tl;
+        arena->recs = recs;
+        for (int64_t L = 0; L <= kMaxQueueLevels; ++L) arena->cap[L] = L <= lv ? cap[L] : 0;
     }
-    const size_t recBytes = (size_t)(arena->levels * arena->tiles * 64) * sizeof(BounceRec);
-    const size_t maskBytes = (size_t)(arena->levels * arena->tiles) * sizeof(unsigned long long);
     char* b = static_cast<char*>(arena->base);
-    P.bounce = reinterpret_cast<BounceRec*>(b);
-    P.bmask = reinterpret_cast<unsigned long long*>(b + recBytes);
-    P.bact = reinterpret_cast<uint32_t*>(b + recBytes + maskBytes);
-    P.bounce_cap = tiles * 64;
-    P.bounce_tiles = (int32_t)tiles;
+    P.qhdr = reinterpret_cast<unsigned long long*>(b);
+    P.bounce = reinterpret_cast<BounceRec*>(b + (size_t)kQHdrWords * 8);
+    P.qneed = arena->by_need ? arena->qneed_dev : nullptr;
+    P.qrecs = arena->recs;
+    P.qlevels = (int32_t)arena->levels;
+    arena->check = arena->by_need;
+    arena->check_levels = levels;
     return true;
+}
+
+// After a by_need arena's render: fold its need into the replica's hint; true when a level
+// overflowed (some of its rays were dropped: the render must run again on a larger arena).
+static bool queue_overflowed(DeviceReplica& r, BounceArena& a) {
+    if (!a.check) return false;
+    a.check = false;
+    bool over = false;
+    for (int64_t L = 1; L <= a.check_levels; ++L) {
+        const int64_t need = (int64_t)a.qneed[L];
+        r.qhint[L] = std::max(r.qhint[L], need);
+        over = over || need > a.cap[L];
+    }
+    return over;
+}
+
+// device.h xcd_tile on the host: block b -> tile of the row-major XCD-group mapping
+static int64_t xcd_tile_host(int64_t b, int64_t nb, int64_t G) {
+    if (G <= 1) return b;
+    const int64_t round = 8 * G, full = nb / round * round;
+    if (b >= full) return b;
+    const int64_t x = b & 7, k = b >> 3;
+    return ((k / G) * 8 + x) * G + (k % G);
+}
+
+// From the measured wave times: the XCD tile groups (G consecutive tiles, device.h xcd_tile) by
+// their slowest tile, the top `pct` % of them first, slowest first, the rest in row-major order;
+// then the same block -> position mapping as xcd_tile, so a group's tiles still share an XCD.
+static int32_t build_tile_order(TileOrder& e, int64_t pct) {
+    const int64_t n = e.n, G = std::max<int64_t>(1, e.key.group);
+    std::vector<unsigned long long> c((size_t)(2 * n));
+    HIP_TRY(hipMemcpy(c.data(), e.cost, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> dur((size_t)n, 0);
+    for (int64_t b = 0; b < n; ++b) {
+        const unsigned long long t0 = c[2 * b], t1 = c[2 * b + 1];
+        dur[(size_t)xcd_tile_host(b, n, G)] = t1 > t0 ? t1 - t0 : 0;
+    }
+    const int64_t ng = n / G;                            // full groups; a partial last group stays last
+    std::vector<unsigned long long> gc((size_t)ng, 0);
+    for (int64_t g = 0; g < ng; ++g)
+        for (int64_t t = g * G; t < g * G + G; ++t) gc[(size_t)g] = std::max(gc[(size_t)g], dur[(size_t)t]);
+    std::vector<int64_t> byc((size_t)ng);
+    for (int64_t g = 0; g < ng; ++g) byc[(size_t)g] = g;
+    std::stable_sort(byc.begin(), byc.end(), [&](int64_t a, int64_t b) { return gc[(size_t)a] > gc[(size_t)b]; });
+    const int64_t npro = (ng * pct + 99) / 100;
+    std::vector<char> pro((size_t)ng, 0);
+    std::vector<uint32_t> seq;
+    seq.reserve((size_t)n);
+    for (int64_t k = 0; k < npro; ++k) {
+        const int64_t g = byc[(size_t)k];
+        pro[(size_t)g] = 1;
+        for (int64_t t = g * G; t < g * G + G; ++t) seq.push_back((uint32_t)t);
+    }
+    for (int64_t g = 0; g < ng; ++g)
+        if (!pro[(size_t)g])
+            for (int64_t t = g * G; t < g * G + G; ++t) seq.push_back((uint32_t)t);
+    for (int64_t t = ng * G; t < n; ++t) seq.push_back((uint32_t)t);
+    std::vector<uint32_t> ord((size_t)n);
+    for (int64_t b = 0; b < n; ++b) ord[(size_t)b] = seq[(size_t)xcd_tile_host(b, n, G)];
+    HIP_TRY(hipMemcpy(e.order, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    e.state = 2;
+    return RT_OK;
+}
+
+// Before a megakernel launch of n blocks: the order of its (camera, chunk selection) when known
+// (P.tile_order), else, the first time, its wave times are recorded (P.tile_cost; the returned
+// entry's event is recorded behind the launch).  Renders while the first one runs use row-major
+// order.  At most kMaxTileOrders selections are kept (least recently used out).
+constexpr size_t kMaxTileOrders = 32;
+static TileOrder* tile_order_for(const rt_scene* s, DeviceReplica& r, RenderParams& P, int64_t n) {
+    const int64_t pct = s->opt[kOptTileOrder];
+    if (pct <= 0 || n < 2) return nullptr;
+    TileOrderKey k{};
+    std::memcpy(k.eye, P.cam.eye, sizeof(k.eye));
+    std::memcpy(k.w, P.cam.w, sizeof(k.w));
+    k.width = P.cam.width; k.height = P.cam.height;
+    k.first = P.chunk_first; k.step = P.chunk_step; k.chunks = P.num_chunks; k.group = P.xcd_remap;
+    TileOrder* e = nullptr;
+    for (TileOrder& o : r.orders)
+        if (o.key == k && o.n == n) { e = &o; break; }
+    if (!e) {
+        if (r.orders.size() >= kMaxTileOrders) {
+            auto lru = std::min_element(r.orders.begin(), r.orders.end(),
+                                        [](const TileOrder& a, const TileOrder& b) { return a.used < b.used; });
+            if (lru->state == 1) return nullptr;              // still being measured: keep it
+            retire(r, lru->order, lru->n * 4); retire(r, lru->cost, lru->n * 16);
+            if (lru->ev) (void)hipEventDestroy(lru->ev);
+            r.orders.erase(lru);
+        }
+        TileOrder o;
+        o.key = k;
+        o.n = n;
+        if (hipMalloc((void**)&o.order, (size_t)n * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc((void**)&o.cost, (size_t)(2 * n) * sizeof(unsigned long long)) != hipSuccess ||
+            hipEventCreateWithFlags(&o.ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(o.order); (void)hipFree(o.cost);
+            return nullptr;
+        }
+        r.orders.push_back(o);
+        e = &r.orders.back();
+    }
+    e->used = ++r.order_clock;
+    if (e->state == 1) {
+        if (hipEventQuery(e->ev) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+        if (build_tile_order(*e, pct) != RT_OK) { (void)hipGetLastError(); e->state = 0; return nullptr; }
+    }
+    if (e->state == 2) { P.tile_order = e->order; return nullptr; }
+    P.tile_cost = e->cost;                                // state 0: this launch measures
+    e->state = 1;
+    return e;
 }
 
 static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P0, hipStream_t stream, bool count,
@@ -1896,35 +2080,36 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     } while (0)
     if (bounce && !count && queue_arena(s, r, arena, P, (int64_t)grid.x * (bt / 64), stream)) {
         // primary + shadow rays of every pixel in the spill-free primary instantiation, then per
-        // level the tile list (k_qscan) and the level's rays in coherent batches (k_bounce)
+        // level the level's rays in coherent batches (k_bounce), then the need (k_queue_done)
+        TileOrder* measuring = tile_order_for(s, r, P, (int64_t)grid.x);
 #define MYRT_QPRIM(W_) hipLaunchKernelGGL((dev::render_kernel<false, false, W_, true>), grid, block, lds, stream, P)
         MYRT_BY_WALK(MYRT_QPRIM);
 #undef MYRT_QPRIM
+        if (measuring) HIP_TRY(hipEventRecord(measuring->ev, stream));
         const dim3 qgrid((unsigned)(r.cus * 4 * MYRT_QUEUE_WPE)), qblock(64);
         const size_t qlds = (size_t)dev::kLds * 64 * sizeof(unsigned long long);
-        const dim3 sgrid((unsigned)((P.bounce_tiles + dev::kQScanTiles - 1) / dev::kQScanTiles));
         // option queue_levels (timing probe only: frames are incomplete below max_depth)
         const int64_t ql = s->opt[kOptQueueLevels];
         const int32_t levels = ql >= 0 ? (int32_t)std::min<int64_t>(ql, P.max_depth) : P.max_depth;
         for (int32_t level = 1; level <= levels; ++level) {
-            hipLaunchKernelGGL(dev::k_qcount, sgrid, dim3(dev::kQScanThreads), 0, stream, P, level);
-            hipLaunchKernelGGL(dev::k_qscan, sgrid, dim3(dev::kQScanThreads), 0, stream, P, level);
 #define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), qgrid, qblock, qlds, stream, P, level)
             MYRT_BY_WALK(MYRT_QB);
 #undef MYRT_QB
         }
-        hipLaunchKernelGGL(dev::k_queue_reset, dim3(256), dim3(256), 0, stream, P, (int)P.max_depth);
+        hipLaunchKernelGGL(dev::k_queue_done, dim3(1), dim3(64), 0, stream, P, (int)P.max_depth);
     } else if (count) {
         const bool u = walk == dev::kWalkIdentity;
         if (bounce) { if (u) MYRT_LAUNCH(true, true, dev::kWalkIdentity); else MYRT_LAUNCH(true, true, dev::kWalkGeneral); }
         else { if (u) MYRT_LAUNCH(true, false, dev::kWalkIdentity); else MYRT_LAUNCH(true, false, dev::kWalkGeneral); }
     } else {
+        TileOrder* measuring = tile_order_for(s, r, P, (int64_t)grid.x);
 #define MYRT_B1(W_) MYRT_LAUNCH(false, true, W_)
 #define MYRT_B0(W_) MYRT_LAUNCH(false, false, W_)
         if (bounce) MYRT_BY_WALK(MYRT_B1);
         else MYRT_BY_WALK(MYRT_B0);
 #undef MYRT_B1
 #undef MYRT_B0
+        if (measuring) HIP_TRY(hipEventRecord(measuring->ev, stream));
     }
 #undef MYRT_BY_WALK
 #undef MYRT_LAUNCH
@@ -2012,11 +2197,14 @@ int32_t rt_scene_info_get(const rt_scene* s, rt_scene_info* out) {
     return RT_OK;
 }
 
-int32_t rt_scene_set_option(rt_scene* s, const char* name, int64_t value) {
+static int32_t set_option(rt_scene* s, const char* name, int64_t value, bool unsafe_ok) {
     if (!s) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
     if (!name) return fail(RT_ERR_INVALID_ARG, "option name is NULL");
     for (int k = 0; k < kOptCount; ++k) {
         if (std::strcmp(name, kOptDefs[k].name) != 0) continue;
+        if (kOptDefs[k].unsafe && !unsafe_ok)
+            return fail(RT_ERR_INVALID_ARG, std::string("option ") + name +
+                                                " is a test hook (rt_scene_set_unsafe_option, not for production)");
         if (value < kOptDefs[k].lo || value > kOptDefs[k].hi)
             return fail(RT_ERR_INVALID_ARG, std::string("option ") + name + " out of range [" +
                                                 std::to_string(kOptDefs[k].lo) + ", " + std::to_string(kOptDefs[k].hi) + "]");
@@ -2025,6 +2213,12 @@ int32_t rt_scene_set_option(rt_scene* s, const char* name, int64_t value) {
         return RT_OK;
     }
     return fail(RT_ERR_INVALID_ARG, std::string("unknown option ") + name);
+}
+
+int32_t rt_scene_set_option(rt_scene* s, const char* name, int64_t value) { return set_option(s, name, value, false); }
+
+int32_t rt_scene_set_unsafe_option(rt_scene* s, const char* name, int64_t value) {
+    return set_option(s, name, value, true);
 }
 
 int32_t rt_scene_get_option(const rt_scene* s, const char* name, int64_t* value) {
@@ -2110,6 +2304,7 @@ int32_t rt_render_device_counted(rt_scene* s, int32_t slot, int32_t cam, int32_t
             out->iter_lane_leaf[k] = (int64_t)c[20 + 5 * k];
         }
     }
+    reclaim(s);
     return RT_OK;
 }
 
@@ -2219,7 +2414,12 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
     const int dma = (int)s->opt[kOptSubmitDma];
     const bool counters_out = s->opt[kOptSubmitCounters] != 0;
     const int64_t fail_at = s->opt[kOptDebugFailReplica];   // test hook
-    auto launch_one = [&](int32_t k) -> int32_t {
+    // replica k's launches, kept by value in the slot (Flight::relaunch): wait_impl runs them again
+    // when the compacted bounce render's arena overflowed
+    auto make_launch = [s, q, qs, first, step, D, H, W, cam, frame, dma, timing, counters_out, concurrent, full_slots,
+                        fail_at, out_rgb, out_rgba8](int32_t k, double* zr, uint8_t* za) -> std::function<int32_t()> {
+      return [s, q, qs, first, step, D, H, W, cam, frame, dma, timing, counters_out, concurrent, full_slots, fail_at,
+              out_rgb, out_rgba8, k, zr, za]() -> int32_t {
         DeviceReplica& r = s->devs[k];
         Flight& f = r.fl[q];
         const int32_t myFirst = first + k * step, myStep = step * D;
@@ -2231,11 +2431,12 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         if (dma) {
             const int64_t px = (int64_t)nq * 8 * W;
             if (px > f.stage_px) {
-                retire(r, f.stage_rgb); retire(r, f.stage_rgba);
+                const int64_t cap = grown(px, f.stage_px);
+                retire(r, f.stage_rgb, f.stage_px * 24); retire(r, f.stage_rgba, f.stage_px * 4);
                 f.stage_rgb = nullptr; f.stage_rgba = nullptr; f.stage_px = 0;
-                HIP_TRY(hipMalloc((void**)&f.stage_rgb, px * 3 * sizeof(double)));
-                HIP_TRY(hipMalloc((void**)&f.stage_rgba, px * 4));
-                f.stage_px = px;
+                HIP_TRY(hipMalloc((void**)&f.stage_rgb, cap * 3 * sizeof(double)));
+                HIP_TRY(hipMalloc((void**)&f.stage_rgba, cap * 4));
+                f.stage_px = cap;
             }
         }
         if (!f.counters_zero) HIP_TRY(hipMemsetAsync(f.counters, 0, kCounterWords * sizeof(unsigned long long), st));
@@ -2243,8 +2444,8 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         f.used = true;                                   // work may be queued on its stream from here on
         if (timing) HIP_TRY(hipEventRecord(f.ev0, st));
         f.timed = timing;
-        RenderParams P = make_params(s, r, cam, myFirst, myStep, dma ? (out_rgb ? f.stage_rgb : nullptr) : zrgb[k],
-                                     dma ? (out_rgba8 ? f.stage_rgba : nullptr) : zrgba[k]);
+        RenderParams P = make_params(s, r, cam, myFirst, myStep, dma ? (out_rgb ? f.stage_rgb : nullptr) : zr,
+                                     dma ? (out_rgba8 ? f.stage_rgba : nullptr) : za);
         P.counters = f.counters;
         if (!dma) {                                      // rows at their places in the caller's buffer
             P.out_first = frame ? 0 : first;
@@ -2284,10 +2485,13 @@ static int32_t submit_impl(rt_scene* s, int32_t cam, int32_t first, int32_t step
         f.counters_zero = counters_out;
         f.counters_valid = counters_out;
         return RT_OK;
+      };
     };
     for (int32_t k = 0; k < D; ++k) {
         if (first + k * step >= num_chunks_total(H)) continue;
-        const int32_t rc = launch_one(k);
+        Flight& fk = s->devs[k].fl[q];
+        fk.relaunch = make_launch(k, zrgb[k], zrgba[k]);
+        const int32_t rc = fk.relaunch();
         if (rc != RT_OK) {
             // replicas already launched write into the caller's buffers: drain them before the
             // error returns (the caller may free the buffers), and leave the slot free
@@ -2335,6 +2539,32 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
     }
     lock.lock();
     fp.waiting = false;
+    // Compacted bounce render: a replica whose by_need arena overflowed (rays were dropped) renders
+    // its share again on an arena grown to the need its render reported; a frame's need does not
+    // change between runs, so one retry suffices (the third check is an error).
+    for (int attempt = 0; e == hipSuccess; ++attempt) {
+        std::vector<std::pair<int, hipEvent_t>> redo;
+        for (auto& r : s->devs) {
+            Flight& f = r.fl[q];
+            if (!f.used || !queue_overflowed(r, f.arena)) continue;
+            if (attempt == 2 || !f.relaunch) {
+                fp.pending = false;
+                return fail(RT_ERR_DEVICE, "compacted bounce queues overflowed again after growing");
+            }
+            const int32_t rc = f.relaunch();
+            if (rc != RT_OK) {
+                (void)hipStreamSynchronize(r.fl[q].stream);
+                fp.pending = false;
+                return rc;
+            }
+            redo.emplace_back(r.device, f.done);
+        }
+        if (redo.empty()) break;
+        for (auto& de : redo) {
+            if (e == hipSuccess) e = hipSetDevice(de.first);
+            if (e == hipSuccess) e = hipEventSynchronize(de.second);
+        }
+    }
     fp.pending = false;
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("render failed: ") + hipGetErrorString(e));
     double km = 0;
@@ -2360,6 +2590,7 @@ static int32_t wait_impl(rt_scene* s, std::unique_lock<std::mutex>& lock, int64_
         stats->rewalked = rw;
         stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - fp.t0).count();
     }
+    reclaim(s);
     return RT_OK;
 }
 
@@ -2469,10 +2700,12 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
         HIP_TRY(hipSetDevice(r.device));
         const int64_t px = (int64_t)pl.rows * W;
         if (!zerocopy && px > r.out_cap_px) {
-            retire(r, r.out_d); retire(r, r.out8_d); r.out_d = nullptr; r.out8_d = nullptr; r.out_cap_px = 0;
-            HIP_TRY(hipMalloc((void**)&r.out_d, px * 3 * sizeof(double)));
-            HIP_TRY(hipMalloc((void**)&r.out8_d, px * 4));
-            r.out_cap_px = px;
+            const int64_t cap = grown(px, r.out_cap_px);
+            retire(r, r.out_d, r.out_cap_px * 24); retire(r, r.out8_d, r.out_cap_px * 4);
+            r.out_d = nullptr; r.out8_d = nullptr; r.out_cap_px = 0;
+            HIP_TRY(hipMalloc((void**)&r.out_d, cap * 3 * sizeof(double)));
+            HIP_TRY(hipMalloc((void**)&r.out8_d, cap * 4));
+            r.out_cap_px = cap;
         }
         if (!direct && px > r.host_cap_px) {
             if (r.host_rgb) (void)hipHostFree(r.host_rgb);
@@ -2658,6 +2891,7 @@ int32_t rt_render_ex(rt_scene* s, int32_t cam, int32_t first, int32_t step, doub
         stats->rewalked = rw;
         stats->milliseconds = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
+    reclaim(s);
     return RT_OK;
 }
 

@@ -622,12 +622,15 @@ struct WideBuilder {
 // profiles/r05b_ab_c3.txt).  The walk then continues with the first slot hit and pushes the others in reverse
 // (wide.h), which replaces the per-node distance sort.  Exactness does not depend on the order
 // (wide.h header: only equal-t candidates depend on it, and those are re-walked in the
-// reference's order).  MYRT_WIDE_ORDER (host build, measurement): 1 = near corners instead of
+// reference's order).  -DMYRT_WIDE_ORDER (compile-time measurement switch, like the other MYRT_*
+// build switches; the product reads no environment variable here): 1 = near corners instead of
 // centres, 2 = slot order kept.
+#ifndef MYRT_WIDE_ORDER
+#define MYRT_WIDE_ORDER 0
+#endif
 static void wide_octant_copies(HostScene& S) {
     const size_t N = S.wnodes.size();
-    const char* env = std::getenv("MYRT_WIDE_ORDER");
-    const int mode = env ? std::atoi(env) : 0;
+    constexpr int mode = MYRT_WIDE_ORDER;
     std::vector<W4Node> out(8 * N);
     const std::vector<W4Node>& in = S.wnodes;
     run_chunks(std::min(8, build_threads()), [&](int k) {
@@ -641,13 +644,13 @@ static void wide_octant_copies(HostScene& S) {
             int perm[4] = {0, 1, 2, 3};
             for (int c = 0; c < 4; ++c) {
                 if (!(a.pnear[0][c] < HUGE_VALF)) { key[c] = HUGE_VAL; continue; }
-                double k = 0.0;
+                double proj = 0.0;
                 for (int ax = 0; ax < 3; ++ax) {
                     const bool neg = (o >> ax) & 1;
                     const double lo = a.pnear[ax][c], hi = a.pfar[ax][c];
-                    k += mode == 1 ? (neg ? -hi : lo) : (neg ? -0.5 : 0.5) * (lo + hi);
+                    proj += mode == 1 ? (neg ? -hi : lo) : (neg ? -0.5 : 0.5) * (lo + hi);
                 }
-                key[c] = mode == 2 ? (double)c : k;
+                key[c] = mode == 2 ? (double)c : proj;
             }
             std::stable_sort(perm, perm + 4, [&](int p, int q) { return key[p] < key[q]; });
             for (int i = 0; i < 4; ++i) {
@@ -786,7 +789,6 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         for (int k = 0; k < 5; ++k) { dst[k][0] = src[k]->x; dst[k][1] = src[k]->y; dst[k][2] = src[k]->z; }
         dm.phong = m.phong; dm.ior = m.ior; dm.absorption_index = m.absorption_index; dm.roughness = m.roughness;
         dm.type = m.type;
-        if (m.type == RT_MAT_DIELECTRIC) S.has_dielectric = true;
         S.mats.push_back(dm);
     }
     for (int i = 0; i < d->num_point_lights; ++i) {
@@ -1210,6 +1212,13 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
         di.kind = bb.kind;
         S.insts.push_back(di);
         S.inst_bvh_hash.push_back(bb.hash);
+        // dielectric frames take the full trace() passes: only when an instance shades with a
+        // dielectric (the clamped material index every hit uses, Object+Extension.swift:104-106, H14) - an
+        // unused dielectric in the material list does not change a frame
+        if (!S.mats.empty()) {
+            const int mi = std::max(0, std::min((int)S.mats.size() - 1, (int)di.material - 1));
+            if (S.mats[mi].type == RT_MAT_DIELECTRIC) S.has_dielectric = true;
+        }
     }
     if (!insts.empty()) {
         RefBVH tb = build_ref_bvh(tp, 2, 12);

@@ -163,6 +163,11 @@ class RayTracerEngine:
     def set_option(self, name: str, value: int):
         _check(load_library().rt_scene_set_option(self._h, name.encode(), int(value)))
 
+    def set_unsafe_option(self, name: str, value: int):
+        """Test hooks (debug_fail_replica, wide_delta_scale) through the non-production
+        rt_scene_set_unsafe_option; set_option refuses them."""
+        _check(load_library().rt_scene_set_unsafe_option(self._h, name.encode(), int(value)))
+
     def get_option(self, name: str) -> int:
         v = C.c_int64()
         _check(load_library().rt_scene_get_option(self._h, name.encode(), C.byref(v)))

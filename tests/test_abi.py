@@ -77,6 +77,7 @@ def test_error_codes_without_compute():
     v = C.c_int64()
     assert lib.rt_scene_set_option(None, b"wide", 0) == A.RT_ERR_NO_SCENE
     assert lib.rt_scene_get_option(None, b"wide", C.byref(v)) == A.RT_ERR_NO_SCENE
+    assert lib.rt_scene_set_unsafe_option(None, b"wide_delta_scale", 0) == A.RT_ERR_NO_SCENE
 
 
 def test_header_declares_the_abi_version_and_struct_sizes():

@@ -157,7 +157,7 @@ def test_failed_replica_launch_drains_and_frees_the_slot():
     want = _sync(eng, 0, 0, 1, H, W)
     out = M.pinned_array((H, W, 4), np.uint8)
     out.fill(0)
-    eng.set_option("debug_fail_replica", 1)
+    eng.set_unsafe_option("debug_fail_replica", 1)
     with pytest.raises(M.RenderError) as e:
         eng.submit_into(0, 0, 1, rgba=out, frame_layout=True)
     assert e.value.code == A.RT_ERR_DEVICE and "injected" in str(e.value)
@@ -170,7 +170,7 @@ def test_failed_replica_launch_drains_and_frees_the_slot():
         rows[8 * c: 8 * c + 8] = True
     snap = out.copy()
     assert np.array_equal(snap[rows], want[1][rows]) and np.all(snap[~rows] == 0)
-    eng.set_option("debug_fail_replica", -1)
+    eng.set_unsafe_option("debug_fail_replica", -1)
     outs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(A.RT_MAX_IN_FLIGHT)]
     ts = [eng.submit_into(0, 0, 1, rgba=o, frame_layout=True) for o in outs]
     for t, o in zip(ts, outs):
@@ -288,4 +288,60 @@ def test_scratch_growth_beside_renders_in_flight():
     rows = _chunk_rows(H, 1, 4)
     assert float(np.abs(small.cpu().numpy()[: rows.sum()] - ref[rows]).max()) <= 1e-5
     assert eng.info().scratch_bytes > 0
+    eng.close()
+
+
+def _mirror_ball(w=160, h=120, depth=3):
+    """A diffuse floor with one mirror sphere over it: a minority of the pixels reflect, and some
+    of their reflected rays hit the sphere's own floor image and stop."""
+    mats = [M.Material(ambient=(0.1, 0.1, 0.1), diffuse=(0.6, 0.7, 0.5), specular=(0.3, 0.3, 0.3), phong=16.0),
+            M.Material(ambient=(0.1, 0.1, 0.1), diffuse=(0.2, 0.2, 0.2), specular=(0.4, 0.4, 0.4), phong=24.0,
+                       mirror=(0.7, 0.7, 0.7), type="mirror")]
+    floor = M.Mesh(id=1, material="1", positions=np.array([[-8, 0, 8], [8, 0, 8], [8, 0, -8], [-8, 0, -8]], np.float64),
+                   indices=np.array([[1, 2, 3], [1, 3, 4]], np.int32), shading_mode="flat")
+    cam = M.Camera(position=(0.0, 3.0, 7.0), gaze_point=(0.0, 0.8, 0.0), up=(0.0, 1.0, 0.0), fovy=45.0,
+                   image_resolution=(w, h))
+    return M.Scene(cameras=[cam], materials=mats,
+                   objects=[floor, M.Sphere(center=(0.4, 1.0, 0.0), radius=1.0, material="2"),
+                            M.Sphere(center=(-1.6, 0.6, 1.2), radius=0.6, material="2")],
+                   point_lights=[M.PointLight((3.0, 6.0, 4.0), (600.0, 600.0, 600.0))],
+                   ambient_light=(15.0, 15.0, 15.0), background_color=(40.0, 60.0, 90.0),
+                   shadow_ray_epsilon=1e-3, intersection_test_epsilon=1e-6, max_recursion_depth=depth)
+
+
+@pytest.mark.parametrize("scene", ["ball", "corridor"])
+def test_bounce_queues_hold_only_the_rays(scene):
+    """Compacted bounce render, records compacted per level: a level holds only its
+    rays, so the 16 in-flight slots' arenas are sized by the rays, not by levels x pixels x 128 B.
+    Each slot's arena starts at the replica's measured need (1/16 of the worst case before any is
+    known): the corridor, where nearly every pixel reflects, overflows that first guess and its
+    frame is rendered again on a grown arena (render.hip wait_impl).  Every frame of three
+    pipelined rounds equals the oracle, and the scratch stops growing after the first round
+    (retired buffers are freed once nothing is in flight)."""
+    from test_gpu_features import _mirror_corridor
+    sc = _mirror_ball() if scene == "ball" else _mirror_corridor(4, 96, 64)
+    W, H = sc.cameras[0].image_resolution
+    ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
+    eng = M.RayTracerEngine(sc)
+    assert eng.get_option("queue") == 1
+    Q = A.RT_MAX_IN_FLIGHT
+    fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
+    submit, wait = eng.frame_pipeline(0, 0, 1, fbs, frame_layout=True)
+    scratch = []
+    for rnd in range(3):
+        for fb in fbs:
+            fb.fill(0)
+        ts = [submit(k) for k in range(Q)]
+        for k, t in enumerate(ts):
+            st = wait(t)
+            assert np.array_equal(fbs[k], ref8), f"round {rnd} frame {k} differs"
+            assert st.secondary_rays == ost.secondary_rays and st.shadow_rays == ost.shadow_rays
+        scratch.append(eng.info().scratch_bytes)
+    levels = sc.max_recursion_depth
+    per_pixel_layout = Q * levels * W * H * 128            # the round-5 arenas: a record per pixel and level
+    print(f"{scene}: scratch {scratch} B; per-pixel layout {per_pixel_layout} B; "
+          f"secondary rays {ost.secondary_rays} of {levels * W * H} slots")
+    assert scratch[1] == scratch[2] and scratch[0] >= scratch[1]
+    if scene == "ball":
+        assert scratch[2] < per_pixel_layout / 4
     eng.close()

@@ -24,6 +24,7 @@ import numpy as np
 import pytest
 
 import myraytracer_amd as M
+from myraytracer_amd import _abi as A
 from myraytracer_amd import scenes
 import oracle
 
@@ -58,7 +59,7 @@ def _far(sc, scale, offset):
 def _engine(sc, permille=None):
     eng = M.RayTracerEngine(sc)
     if permille is not None:
-        eng.set_option("wide_delta_scale", permille)
+        eng.set_unsafe_option("wide_delta_scale", permille)
     assert eng.get_option("wide") == 1
     return eng
 
@@ -236,6 +237,26 @@ def test_translated_c3_full_frame():
     assert np.array_equal(rgba, ref8), f"RGBA8 differs on {int((rgba != ref8).any(-1).sum())} px"
     assert float(np.abs(rgb - ref).max()) <= TOL
     assert st.primary_rays == ost.primary_rays and st.shadow_rays_traced == ost.shadow_rays_used
+
+
+def test_test_hooks_are_refused_by_the_production_entry_point():
+    """wide_delta_scale (voids the exactness proof below 1000) and debug_fail_replica (injects
+    failures) are test hooks: rt_scene_set_option refuses them with RT_ERR_INVALID_ARG and leaves
+    the option at its production value; only rt_scene_set_unsafe_option (ABI 4, not for
+    production) sets them.  Every ordinary option still goes through rt_scene_set_option."""
+    eng = M.RayTracerEngine(scenes.scene_c1(16, 16))
+    for name, val, default in (("wide_delta_scale", 0, 1000), ("wide_delta_scale", 1000, 1000),
+                               ("debug_fail_replica", 0, -1)):
+        with pytest.raises(M.RenderError) as e:
+            eng.set_option(name, val)
+        assert e.value.code == A.RT_ERR_INVALID_ARG and "test hook" in str(e.value)
+        assert eng.get_option(name) == default
+    eng.set_unsafe_option("wide_delta_scale", 500)
+    assert eng.get_option("wide_delta_scale") == 500
+    eng.set_unsafe_option("wide_delta_scale", 1000)
+    eng.set_option("queue", 0)                               # an ordinary option
+    assert eng.get_option("queue") == 0
+    eng.close()
 
 
 def test_the_sets_reach_the_bound():

@@ -10,7 +10,7 @@ KX=""
 case "$cfg" in
   # C5 (render option queue = 1): the queued primary pass + the per-level launches of its frame
   c5) K="${KERNEL:-render_kernel<false, false, 1, true>}"
-      KX="--extra-kernel k_qcount --extra-kernel k_qscan --extra-kernel 'k_bounce<1>' --extra-kernel k_queue_reset" ;;
+      KX="--extra-kernel 'k_bounce<1>' --extra-kernel k_queue_done" ;;
   *)  K="${KERNEL:-render_kernel<false, false, 1, false>}" ;;
 esac
 B="python3 bench.py --config $cfg --steps $steps --warmup $warm --no-cpu-baseline --no-side-paths"

@@ -22,7 +22,7 @@ lib_sha256_16 ties the summary to the library build it measured (bench.py checks
 
 Frame chains (--kernel given more than once; the first names the frame's first kernel): a frame
 that runs several launches (C5's compacted bounce render: the queued primary pass, then per level
-k_qcount / k_qscan / k_bounce, then k_queue_reset) is summarised per FRAME: frames = dispatches of
+k_bounce, then k_queue_done; round 5: k_qcount / k_qscan per level too) is summarised per FRAME: frames = dispatches of
 the first kernel; every counter is summed over all dispatches of the listed kernels and divided by
 the frames; kernel_ms = the listed kernels' total duration per frame; busy / utilisation ratios
 divide the chain's summed counters.  `chain` lists each kernel's share.
