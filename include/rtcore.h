@@ -210,6 +210,9 @@ int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
  *   deep_cap_mb (8192)   deep trace() frames per launch batch
  *   batches (0 = auto), zerocopy (1)            rt_render delivery
  *   submit_events (1), submit_counters (1), submit_dma (0)   rt_render_submit delivery
+ *   tile_order (0)       % of tile groups dispatched slowest first
+ *   fit (1)              transformed scenes: the flattened instance tree (wide.h fit_walk);
+ *                        0 = the TLAS / per-BLAS four-wide walk (tw_walk)
  * Unknown names and out-of-range values return RT_ERR_INVALID_ARG.  Set options between
  * renders (not while renders of the scene are in flight).  The test hooks below are refused
  * here (RT_ERR_INVALID_ARG); rt_scene_get_option reads every option. */

@@ -819,7 +819,7 @@ __device__ __forceinline__ void uni_closest(const RenderParams& P, const V3& o, 
     h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
     if (WIDE && !MYRT_REF(P) && P.wide && __all(wide_ok(inv))) {
         bool tie = false;
-        (void)wide_walk<COUNT, false>(P, o, d, inv, tlo, DINF, h, tie, st, c);
+        (void)wide_walk<COUNT, false>(P, TwWorld{o, d}, inv, tlo, DINF, h, tie, st, c);
 #ifndef MYRT_REWALK
 #define MYRT_REWALK 1
 #endif
@@ -856,14 +856,15 @@ __device__ __forceinline__ bool uni_occluded(const RenderParams& P, const V3& o,
     if (WIDE && !MYRT_REF(P) && P.wide && __all(wide_ok(inv))) {
         Hit hu;
         bool tie = false;
-        return wide_walk<COUNT, true>(P, o, d, inv, 0.0, tmax, hu, tie, st, c);
+        return wide_walk<COUNT, true>(P, TwWorld{o, d}, inv, 0.0, tmax, hu, tie, st, c);
     }
     if (__all(finite3(inv))) return uni_occluded_walk<COUNT, true>(P, o, d, inv, tmax, st, c);
     return uni_occluded_walk<COUNT, false>(P, o, d, inv, tmax, st, c);
 }
 
 // Walks of the render kernels (render.hip WALK template argument)
-constexpr int kWalkGeneral = 0, kWalkIdentity = 1, kWalkTransformed = 2;
+// kWalkFit = transformed scenes through their flattened instance tree (wide.h fit_walk, option fit)
+constexpr int kWalkGeneral = 0, kWalkIdentity = 1, kWalkTransformed = 2, kWalkFit = 3;
 
 // ------------------------------------------------------- unified transformed walk (UT)
 // Scenes whose instances carry transforms or motion (every object of a reference scene is an

@@ -96,6 +96,14 @@ struct DWideInst {
 };
 static_assert(sizeof(DWideInst) == 64, "DWideInst is 64 B");
 
+// Flattened instance tree of a transformed scene (scene.cpp build_fit, wide.h fit_walk): one
+// world-space four-wide tree over every (instance, BLAS leaf run) pair; its terminal slot ~p names
+// pair p: the leaf run's first TriRec (shared by the instances of one mesh) and the instance.
+struct DFitPair {
+    int32_t t0;
+    int32_t inst;
+};
+
 struct DMaterial {        // ParsingKit Material fields used by trace()
     double ambient[3], diffuse[3], specular[3], mirror[3], absorption[3];
     double phong, ior, absorption_index, roughness;
@@ -272,6 +280,11 @@ struct RenderParams {
     // wave (s_memrealtime), recorded by the first render of a camera and chunk selection
     const uint32_t* tile_order;
     unsigned long long* tile_cost;
+    // flattened instance tree (wide.h fit_walk; option fit): its root node in the same node array
+    // and the (leaf run, instance) pairs its terminal slots name; fit == 0: tw_walk
+    const DFitPair* fpairs;
+    int32_t fit_root;
+    int32_t fit;
 };
 
 constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters

@@ -59,12 +59,39 @@ __device__ MYRT_TW_INLINE bool ut_occluded_call(const RenderParams& P, const V3 
     return ut_walk<true>(P, o, d, rcp(d), 0.0, tmax, time, hu, st);
 }
 
+// The flattened instance tree's fallbacks (equal-t ties, world rays out of the FP32 range): the
+// reference-order transformed walk.  (Out of line, __noinline__, the megakernel went to 212 VGPRs
+// and 144 spills: a call costs the kernel its register budget.)
+__device__ __forceinline__ void fit_closest_fallback(const RenderParams& P, const V3 o, const V3 d, double tlo, double time,
+                                                  Hit& h, Stack& st) {
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    (void)ut_walk<false>(P, o, d, rcp(d), tlo, DINF, time, h, st);
+}
+__device__ __forceinline__ bool fit_occluded_fallback(const RenderParams& P, const V3 o, const V3 d, double tmax,
+                                                   double time, Stack& st) {
+    Hit hu;
+    return ut_walk<true>(P, o, d, rcp(d), 0.0, tmax, time, hu, st);
+}
+
 // Closest hit of one ray by the scene's walk (WALK, render_kernel).
 template <bool COUNT, int WALK, bool WIDE = true>
 __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
                                              double time, Hit& h, Stack& st, Counts& c) {
     if (WALK == kWalkIdentity) {
         uni_closest<COUNT, WIDE>(P, o, d, inv, tlo, h, st, c);
+    } else if (WALK == kWalkFit) {
+        h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+        if (WIDE && __all(wide_ok(inv))) {
+            // the flattened instance tree (wide.h fit_walk); equal-t candidates re-walked in order
+            bool tie = false;
+            (void)wide_walk<COUNT, false, true>(P, TwWorld{o, d}, inv, tlo, DINF, h, tie, st, c);
+            if (__any(tie) && tie) {
+                c.ties++;
+                fit_closest_fallback(P, o, d, tlo, time, h, st);
+            }
+            return;
+        }
+        fit_closest_fallback(P, o, d, tlo, time, h, st);
     } else if (WALK == kWalkTransformed) {
         h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
         if (WIDE && P.wide && P.winst && __all(wide_ok(inv))) {
@@ -106,11 +133,44 @@ __device__ __forceinline__ void walk_closest_tw_parked(const RenderParams& P, co
     (void)ut_walk<false>(P, pk.o(), pk.d(), rcp(pk.d()), tlo, DINF, time, h, st);
 }
 
+// ... and through the flattened instance tree (kWalkFit): the walk reads the parked world ray back
+// at each pair, where it forms the local ray
+template <bool COUNT, class Park>
+__device__ __forceinline__ void walk_closest_fit_parked(const RenderParams& P, const Park& pk, double tlo,
+                                                        double time, Hit& h, Stack& st, Counts& c) {
+    h.t = DINF; h.inst = -1; h.tri = -1; h.u = 0; h.v = 0;
+    if (__all(wide_ok(rcp(pk.d())))) {
+        bool tie = false;
+        (void)wide_walk<COUNT, false, true>(P, pk, rcp(pk.d()), tlo, DINF, h, tie, st, c);
+        if (__any(tie) && tie) {
+            c.ties++;
+            fit_closest_fallback(P, pk.o(), pk.d(), tlo, time, h, st);
+        }
+        return;
+    }
+    fit_closest_fallback(P, pk.o(), pk.d(), tlo, time, h, st);
+}
+
 // Any hit of one shadow ray (tMin 0, tMax) by the scene's walk.
 template <bool COUNT, int WALK, bool WIDE = true, bool PARK = (MYRT_TW_PARK != 0), class WPark = TwParked>
 __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o, const V3& d, double tmax, double time,
                                               Stack& st, Counts& c) {
     if (WALK == kWalkIdentity) return uni_occluded<COUNT, WIDE>(P, o, d, tmax, st, c);
+    if (WALK == kWalkFit) {
+        if (!P.has_tlas) return false;
+        Hit hu;
+        const V3 inv = rcp(d);
+        if (WIDE && __all(wide_ok(inv))) {
+            bool tie = false;
+            if (PARK) {
+                WPark pk;                                 // private memory, or the megakernel's LDS slots
+                pk.store(o, d);
+                return wide_walk<COUNT, true, true>(P, pk, inv, 0.0, tmax, hu, tie, st, c);
+            }
+            return wide_walk<COUNT, true, true>(P, TwWorld{o, d}, inv, 0.0, tmax, hu, tie, st, c);
+        }
+        return fit_occluded_fallback(P, o, d, tmax, time, st);
+    }
     if (WALK == kWalkTransformed) {
         if (!P.has_tlas) return false;
         Hit hu;
@@ -355,10 +415,11 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         const V3 inv = rcp(d);
         Hit h;
         park();
-        if (WALK == kWalkTransformed && MYRT_TW_PARK && (!BOUNCE || MYRT_BOUNCE_WIDE)) {
+        if ((WALK == kWalkTransformed || WALK == kWalkFit) && MYRT_TW_PARK && (!BOUNCE || MYRT_BOUNCE_WIDE)) {
             TwPark pk;                                    // the world ray waits in private memory / LDS
             pk.store(o, d);
-            walk_closest_tw_parked<COUNT>(P, pk, tlo, time, h, st, c);
+            if (WALK == kWalkFit) walk_closest_fit_parked<COUNT>(P, pk, tlo, time, h, st, c);
+            else walk_closest_tw_parked<COUNT>(P, pk, tlo, time, h, st, c);
             o = pk.o();
             d = pk.d();
         } else {
@@ -981,6 +1042,7 @@ __global__ __launch_bounds__(256) void k_trace_rays(RenderParams P, RayBatch B) 
     if (P.has_tlas) {
         if (B.uni == 1) uni_closest<false>(P, o, d, rcp(d), B.tlim[i], h, st, c);
         else if (B.uni == 2) walk_closest<false, kWalkTransformed>(P, o, d, rcp(d), B.tlim[i], time, h, st, c);
+        else if (B.uni == 3) walk_closest<false, kWalkFit>(P, o, d, rcp(d), B.tlim[i], time, h, st, c);
         else intersect_closest<false>(P, o, d, rcp(d), B.tlim[i], time, h, st, c);
     }
     V3 p = v3(0, 0, 0), n = v3(0, 0, 0);
@@ -999,6 +1061,7 @@ __global__ __launch_bounds__(256) void k_occluded_rays(RenderParams P, RayBatch 
     const V3 o = v3(B.o[3 * i], B.o[3 * i + 1], B.o[3 * i + 2]), d = v3(B.d[3 * i], B.d[3 * i + 1], B.d[3 * i + 2]);
     const bool hit = B.uni == 1 ? uni_occluded<false>(P, o, d, B.tlim[i], st, c)
                      : B.uni == 2 ? walk_occluded<false, kWalkTransformed, true, false>(P, o, d, B.tlim[i], B.time[i], st, c)
+                     : B.uni == 3 ? walk_occluded<false, kWalkFit, true, false>(P, o, d, B.tlim[i], B.time[i], st, c)
                            : occluded<false>(P, o, d, B.tlim[i], B.time[i], st, c);
     B.out_occ[i] = hit ? 1 : 0;
 }
@@ -1125,6 +1188,7 @@ struct DeviceReplica {
     TriRec* tris = nullptr;
     W4Node* wnodes = nullptr;                 // conservative four-wide walk (wide.h)
     DWideInst* winst = nullptr;               // ... of transformed scenes: per instance (tw_walk)
+    DFitPair* fpairs = nullptr;               // ... their flattened instance tree's pairs (fit_walk)
     double* lbox = nullptr;
     double* normals = nullptr;
     DInstance* insts = nullptr;
@@ -1174,7 +1238,7 @@ enum OptId {
     kOptWide, kOptUnified, kOptUnifiedTransformed, kOptCompactRecords, kOptCompactTris, kOptXcdGroup,
     kOptQueue, kOptQueueLevels, kOptHitlog, kOptNodeshade, kOptLevels, kOptTreePpw, kOptFullFlights,
     kOptDeepCapMb, kOptBatches, kOptZerocopy, kOptSubmitEvents, kOptSubmitCounters, kOptSubmitDma,
-    kOptDebugFailReplica, kOptWideDeltaScale, kOptNodeLists, kOptTileOrder, kOptCount
+    kOptDebugFailReplica, kOptWideDeltaScale, kOptNodeLists, kOptTileOrder, kOptFit, kOptCount
 };
 // `unsafe` options are test hooks: rt_scene_set_option refuses them (RT_ERR_INVALID_ARG); only the
 // non-production entry point rt_scene_set_unsafe_option sets them (rtcore.h).
@@ -1205,6 +1269,7 @@ static const OptDef kOptDefs[kOptCount] = {
                                                      // exactness proof (tests show that it has teeth)
     {"node_lists", 1, 0, 1},              // level passes past 0 and node shading over compacted node lists
     {"tile_order", 0, 0, 100},            // % of XCD tile groups dispatched first, slowest first (TileOrder; 0 = row-major)
+    {"fit", 1, 0, 1},                     // transformed scenes: the flattened instance tree (wide.h fit_walk; 0 = tw_walk)
 };
 
 struct rt_scene {
@@ -1305,7 +1370,7 @@ static void free_replica(DeviceReplica& r) {
     (void)hipSetDevice(r.device);
     (void)hipDeviceSynchronize();
     free_retired(r);
-    (void)hipFree(r.wnodes); (void)hipFree(r.lbox); (void)hipFree(r.winst);
+    (void)hipFree(r.wnodes); (void)hipFree(r.lbox); (void)hipFree(r.winst); (void)hipFree(r.fpairs);
     (void)hipFree(r.recs); (void)hipFree(r.crecs); (void)hipFree(r.ctris); (void)hipFree(r.tris); (void)hipFree(r.normals); (void)hipFree(r.insts);
     (void)hipFree(r.tlas_leaf); (void)hipFree(r.mats); (void)hipFree(r.plights); (void)hipFree(r.counters);
     (void)hipFree(r.alights); (void)hipFree(r.jitter); (void)hipFree(r.wave_times);
@@ -1394,6 +1459,7 @@ static int32_t make_replica(const HostScene& S, int device, DeviceReplica& r, co
         if ((rc = upload(S.lbox, &r.lbox, r.bytes)) != RT_OK) return rc;
     }
     if ((rc = upload(S.winst, &r.winst, r.bytes)) != RT_OK) return rc;
+    if ((rc = upload(S.fpairs, &r.fpairs, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.insts, &r.insts, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.tlas_leaf, &r.tlas_leaf, r.bytes)) != RT_OK) return rc;
     if ((rc = upload(S.mats, &r.mats, r.bytes)) != RT_OK) return rc;
@@ -1548,20 +1614,28 @@ static double dist_to_center(const HostScene& S, const double p[3]) {
 // shadowRayEpsilon; triangle hit points only: scene.cpp build_wide builds no tree for scenes with
 // spheres or planes, whose hit points can lie outside every box).  wdelta = 8 * 2^-24 * max(|box coordinate|, |origin coordinate|) bounds the
 // FP32 rounding of the slab terms (wide.h header); weps = eps rounded down to float.
+// Transformed scenes with a flattened instance tree (option fit): R also covers the tree's
+// magnitudes (fit_coord) and wdelta carries 2^-27 R more for the world <-> local rounding (wide.h
+// fit_walk header); the larger widening only loosens tw_walk's TLAS filter.
 static void set_wide(const HostScene& S, const DeviceReplica& r, RenderParams& P, double origin_coord, bool on,
-                     int64_t scale_permille) {
+                     int64_t scale_permille, bool fit) {
     P.wnodes = r.wnodes; P.lbox = r.lbox; P.wide_root = S.wide_root;
     P.wide_copy_bytes = (uint32_t)(S.wide_copy * (int64_t)sizeof(W4Node));
     P.winst = S.winst.empty() ? nullptr : r.winst;          // transformed scenes (wide.h tw_walk)
     P.tw_tlas_nodes = (int32_t)S.tw_tlas_nodes;
     P.tw_wscale = (float)((double)scale_permille * 1e-3);
-    const double R = std::max(S.wide_coord, origin_coord) + std::fabs(S.shadow_eps) + std::fabs(S.eps);
-    P.wdelta = R * 0x1p-21 * ((double)scale_permille * 1e-3);
+    const bool has_fit = S.fit_root >= 0 && !S.fpairs.empty() && r.fpairs;
+    const double R = std::max({S.wide_coord, has_fit ? S.fit_coord : 0.0, origin_coord}) + std::fabs(S.shadow_eps) +
+                     std::fabs(S.eps);
+    P.wdelta = R * (has_fit ? 0x1p-21 + 0x1p-27 : 0x1p-21) * ((double)scale_permille * 1e-3);
     float we = (float)S.eps;
     if ((double)we > S.eps) we = std::nextafter(we, -HUGE_VALF);
     P.weps = we;
     P.wide = (S.wide_root >= 0 && r.wnodes && !S.has_special && R < 0x1p27 && R > 0x1p-60 && std::isfinite(R) &&
               on) ? 1 : 0;
+    P.fpairs = has_fit ? r.fpairs : nullptr;
+    P.fit_root = has_fit ? S.fit_root : -1;
+    P.fit = (P.wide && has_fit && fit) ? 1 : 0;
 }
 
 static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32_t cam, int32_t first, int32_t step,
@@ -1621,7 +1695,7 @@ static RenderParams make_params(const rt_scene* s, const DeviceReplica& r, int32
         const rt_camera& cam0 = S.cams[cam];
         const double ce[3] = {cam0.position.x, cam0.position.y, cam0.position.z};
         set_wide(S, r, P, std::max({std::fabs(ce[0]), std::fabs(ce[1]), std::fabs(ce[2])}) + std::fabs(cam0.aperture_size),
-                 s->opt[kOptWide] != 0, s->opt[kOptWideDeltaScale]);
+                 s->opt[kOptWide] != 0, s->opt[kOptWideDeltaScale], s->opt[kOptFit] != 0);
     }
     return P;
 }
@@ -1694,10 +1768,11 @@ static int32_t launch_full(const rt_scene* s, DeviceReplica& r, FullScratch& fs,
     }
     const bool unified = P.has_tlas && !P.count_ref && s->opt[kOptUnified] != 0;
     const int walk = (unified && P.identity) ? dev::kWalkIdentity
-                     : (unified && P.ut && !count) ? dev::kWalkTransformed : dev::kWalkGeneral;
+                     : (unified && P.ut && !count) ? (P.fit ? dev::kWalkFit : dev::kWalkTransformed) : dev::kWalkGeneral;
 #define MYRT_BY_WALK(M_)                                                    \
     do {                                                                    \
         if (walk == dev::kWalkIdentity) M_(dev::kWalkIdentity);             \
+        else if (walk == dev::kWalkFit) M_(dev::kWalkFit);                  \
         else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
         else M_(dev::kWalkGeneral);                                         \
     } while (0)
@@ -2070,11 +2145,12 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
     // allow one stack or for counting launches (reference-order counting needs the general walk)
     const bool unified = P.has_tlas && !P.count_ref && s->opt[kOptUnified] != 0;
     const int walk = (unified && P.identity) ? dev::kWalkIdentity
-                     : (unified && P.ut && !count) ? dev::kWalkTransformed : dev::kWalkGeneral;
+                     : (unified && P.ut && !count) ? (P.fit ? dev::kWalkFit : dev::kWalkTransformed) : dev::kWalkGeneral;
 #define MYRT_LAUNCH(C_, B_, W_) hipLaunchKernelGGL((dev::render_kernel<C_, B_, W_>), grid, block, lds, stream, P)
 #define MYRT_BY_WALK(M_)                                                    \
     do {                                                                    \
         if (walk == dev::kWalkIdentity) M_(dev::kWalkIdentity);             \
+        else if (walk == dev::kWalkFit) M_(dev::kWalkFit);                  \
         else if (walk == dev::kWalkTransformed) M_(dev::kWalkTransformed);  \
         else M_(dev::kWalkGeneral);                                         \
     } while (0)
@@ -3005,12 +3081,12 @@ static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o,
         P.fast_rcp = fast_rcp_for(s->host, 2.0 * dm + 1.0);
         double oc = 0.0;                      // the wide walk's widening for these origins
         for (int32_t k = 0; k < 3 * n; ++k) oc = std::isfinite(o[k]) ? std::max(oc, std::fabs(o[k])) : HUGE_VAL;
-        set_wide(s->host, r, P, oc, s->opt[kOptWide] != 0, s->opt[kOptWideDeltaScale]);
+        set_wide(s->host, r, P, oc, s->opt[kOptWide] != 0, s->opt[kOptWideDeltaScale], s->opt[kOptFit] != 0);
     }
     dev::RayBatch B{};
     B.n = n;
     const bool unified = P.has_tlas && s->opt[kOptUnified] != 0;
-    B.uni = (unified && P.identity) ? 1 : (unified && P.ut) ? 2 : 0;   // the render kernels' walk
+    B.uni = (unified && P.identity) ? 1 : (unified && P.ut) ? (P.fit ? 3 : 2) : 0;   // the render kernels' walk
     std::vector<void*> allocs;
     auto dalloc = [&](size_t bytes, void** p) -> int32_t {
         HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 8)));

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 #include <atomic>
 #include <limits>
@@ -701,6 +702,242 @@ static void build_wide(HostScene& S) {
     wide_octant_copies(S);
 }
 
+// Flattened instance tree (transformed scenes; wide.h fit_walk).  One four-wide tree in WORLD
+// space over every (instance, BLAS leaf run) pair, built by binned SAH over the pairs' world boxes
+// (split in two, each half in two again: up to four slots a node), so that the terrain's leaves
+// and the sphere instances' leaves interleave in one walk as an identity scene's do.  A pair's
+// box is AABB.transformed (AABB.swift:71-92) of its local leaf box: the eight corners through
+// localToWorld, min/max.  The walk tests the reference's boxes exactly (FP64) before it accepts a
+// candidate: the instance's TLAS leaf box with the world ray, its BLAS root box and the leaf box
+// with the local ray (RTContext.swift:632-673, 567-571), so the tree only has to be a superset
+// filter: a triangle the reference tests lies in a pair whose world box the walk enters (wide.h
+// fit_walk header: the widening covers the world <-> local rounding while the transforms'
+// condition number stays below kFitKappa; above it the scene keeps tw_walk only).
+constexpr double kFitKappa = 4096.0;
+static double m3_inf_norm(const double* M) {      // column-major 4x4: the 3x3 part's max row sum
+    double n = 0.0;
+    for (int r = 0; r < 3; ++r) n = std::fmax(n, std::fabs(M[r]) + std::fabs(M[4 + r]) + std::fabs(M[8 + r]));
+    return n;
+}
+// min / max of the builder's finite values: plain compares (std::fmin/fmax are libm calls here)
+static inline double fmn(double a, double b) { return b < a ? b : a; }
+static inline double fmx(double a, double b) { return b > a ? b : a; }
+static void build_fit(HostScene& S) {
+    const auto t_start = std::chrono::steady_clock::now();
+    S.fpairs.clear(); S.fit_root = -1; S.fit_nodes = 0; S.fit_depth = 0; S.fit_coord = 0.0;
+    struct Item { double lo[3], hi[3], c[3]; int32_t t0, inst; };
+    std::vector<Item> items;
+    double coord = 0.0;
+    // leaf runs of each BLAS (local boxes), by BLAS root ref
+    std::vector<std::pair<int32_t, std::vector<Item>>> leaves;
+    for (size_t k = 0; k < S.insts.size(); ++k) {
+        const DInstance& I = S.insts[k];
+        const double ka = m3_inf_norm(I.l2w) * m3_inf_norm(I.w2l);
+        if (!(ka <= kFitKappa)) return;
+        const std::vector<Item>* L = nullptr;
+        for (const auto& x : leaves) if (x.first == I.root_ref) { L = &x.second; break; }
+        if (!L) {
+            std::vector<Item> out;
+            auto leaf = [&](int32_t ref, const double* lo, const double* hi) {
+                Item it{};
+                for (int a = 0; a < 3; ++a) { it.lo[a] = lo[a]; it.hi[a] = hi[a]; }
+                it.t0 = ~ref;
+                out.push_back(it);
+            };
+            if (I.root_ref < 0) {
+                leaf(I.root_ref, I.root_lo, I.root_hi);
+            } else {
+                std::vector<int32_t> st{I.root_ref};
+                while (!st.empty()) {
+                    const WRec& r = S.recs[st.back()];
+                    st.pop_back();
+                    for (int c = 0; c < 2; ++c) {
+                        if (r.ref[c] < 0) leaf(r.ref[c], r.lo[c], r.hi[c]);
+                        else st.push_back(r.ref[c]);
+                    }
+                }
+            }
+            leaves.push_back({I.root_ref, std::move(out)});
+            L = &leaves.back().second;
+        }
+        const double nl = m3_inf_norm(I.l2w);
+        for (int a = 0; a < 3; ++a) coord = fmx(coord, std::fabs(I.l2w[12 + a]));
+        for (const Item& x : *L) {
+            Item w{};
+            w.t0 = x.t0;
+            w.inst = (int32_t)k;
+            for (int a = 0; a < 3; ++a) { w.lo[a] = kInf; w.hi[a] = -kInf; }
+            double lc = 0.0;
+            for (int q = 0; q < 8; ++q) {
+                const double p[3] = {(q & 1) ? x.hi[0] : x.lo[0], (q & 2) ? x.hi[1] : x.lo[1], (q & 4) ? x.hi[2] : x.lo[2]};
+                for (int a = 0; a < 3; ++a) {
+                    lc = fmx(lc, std::fabs(p[a]));
+                    const double v = I.l2w[a] * p[0] + I.l2w[4 + a] * p[1] + I.l2w[8 + a] * p[2] + I.l2w[12 + a];
+                    w.lo[a] = fmn(w.lo[a], v);
+                    w.hi[a] = fmx(w.hi[a], v);
+                }
+            }
+            coord = fmx(coord, nl * lc);
+            for (int a = 0; a < 3; ++a) {
+                coord = fmx(coord, fmx(std::fabs(w.lo[a]), std::fabs(w.hi[a])));
+                w.c[a] = 0.5 * w.lo[a] + 0.5 * w.hi[a];
+            }
+            items.push_back(w);
+        }
+    }
+    if (items.empty() || !std::isfinite(coord) || items.size() >= (size_t(1) << 30)) return;
+    // binned SAH split of items [a, b) into [a, m), [m, b) (object median when no bin split helps);
+    // one pass bins all three axes
+    constexpr int kBins = 16;
+    auto split = [&](size_t a, size_t b) -> size_t {
+        double cl[3] = {kInf, kInf, kInf}, ch[3] = {-kInf, -kInf, -kInf};
+        for (size_t i = a; i < b; ++i)
+            for (int x = 0; x < 3; ++x) { cl[x] = fmn(cl[x], items[i].c[x]); ch[x] = fmx(ch[x], items[i].c[x]); }
+        double sc[3];
+        for (int x = 0; x < 3; ++x) sc[x] = ch[x] > cl[x] ? kBins / (ch[x] - cl[x]) : 0.0;
+        int cnt[3][kBins] = {};
+        double blo[3][kBins][3], bhi[3][kBins][3];
+        for (int x = 0; x < 3; ++x)
+            for (int q = 0; q < kBins; ++q)
+                for (int y = 0; y < 3; ++y) { blo[x][q][y] = kInf; bhi[x][q][y] = -kInf; }
+        for (size_t i = a; i < b; ++i) {
+            const Item& it = items[i];
+            for (int x = 0; x < 3; ++x) {
+                const int q = std::min(kBins - 1, (int)((it.c[x] - cl[x]) * sc[x]));
+                cnt[x][q]++;
+                for (int y = 0; y < 3; ++y) {
+                    blo[x][q][y] = fmn(blo[x][q][y], it.lo[y]);
+                    bhi[x][q][y] = fmx(bhi[x][q][y], it.hi[y]);
+                }
+            }
+        }
+        double best = kInf;
+        int bax = -1, bb = 0;
+        for (int x = 0; x < 3; ++x) {
+            if (!(ch[x] > cl[x])) continue;
+            double ra[kBins];
+            {
+                double lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
+                int n = 0;
+                for (int q = kBins - 1; q >= 1; --q) {
+                    n += cnt[x][q];
+                    for (int y = 0; y < 3; ++y) { lo[y] = fmn(lo[y], blo[x][q][y]); hi[y] = fmx(hi[y], bhi[x][q][y]); }
+                    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+                    ra[q] = n ? n * (dx * dy + dy * dz + dz * dx) : 0.0;
+                }
+            }
+            double lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
+            int n = 0;
+            for (int q = 0; q < kBins - 1; ++q) {
+                n += cnt[x][q];
+                for (int y = 0; y < 3; ++y) { lo[y] = fmn(lo[y], blo[x][q][y]); hi[y] = fmx(hi[y], bhi[x][q][y]); }
+                if (n == 0 || n == (int)(b - a)) continue;
+                const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+                const double cost = n * (dx * dy + dy * dz + dz * dx) + ra[q + 1];
+                if (cost < best) { best = cost; bax = x; bb = q; }
+            }
+        }
+        if (bax < 0) return a + (b - a) / 2;
+        const double s0 = sc[bax], c0 = cl[bax];
+        auto mid = std::partition(items.begin() + (ptrdiff_t)a, items.begin() + (ptrdiff_t)b, [&](const Item& it) {
+            return std::min(kBins - 1, (int)((it.c[bax] - c0) * s0)) <= bb;
+        });
+        const size_t m = (size_t)(mid - items.begin());
+        return (m == a || m == b) ? a + (b - a) / 2 : m;
+    };
+    // A subtree: its nodes in preorder (node refs local to `nodes`, terminal slots ~index into `pairs`).
+    // The top two levels build their subtrees on threads of their own, into their own FitOut, and
+    // the parent appends them in slot order: the result does not depend on scheduling.
+    struct FitOut {
+        std::vector<W4Node> nodes;
+        std::vector<DFitPair> pairs;
+        int64_t depth = 0;
+    };
+    std::function<void(size_t, size_t, int64_t, FitOut&, int)> node = [&](size_t a, size_t b, int64_t depth, FitOut& out,
+                                                                         int par) {
+        out.depth = std::max(out.depth, depth);
+        size_t cut[5] = {a, a, b, b, b};
+        int nc;
+        if (b - a <= 4) {
+            nc = (int)(b - a);
+            for (int c = 0; c <= nc; ++c) cut[c] = a + (size_t)c;
+        } else {
+            const size_t m = split(a, b);
+            const size_t m0 = (m - a >= 2) ? split(a, m) : m;
+            const size_t m1 = (b - m >= 2) ? split(m, b) : b;
+            nc = 0;
+            cut[nc++] = a;
+            if (m0 != m) cut[nc++] = m0;
+            cut[nc++] = m;
+            if (m1 != b) cut[nc++] = m1;
+            cut[nc] = b;
+        }
+        const size_t idx = out.nodes.size();
+        out.nodes.emplace_back();
+        int32_t refs[4] = {0, 0, 0, 0};
+        double blo[4][3], bhi[4][3];
+        FitOut sub[4];
+        std::vector<std::thread> th;
+        for (int c = 0; c < nc; ++c) {
+            for (int y = 0; y < 3; ++y) { blo[c][y] = kInf; bhi[c][y] = -kInf; }
+            for (size_t i = cut[c]; i < cut[c + 1]; ++i)
+                for (int y = 0; y < 3; ++y) { blo[c][y] = fmn(blo[c][y], items[i].lo[y]); bhi[c][y] = fmx(bhi[c][y], items[i].hi[y]); }
+            if (cut[c + 1] - cut[c] == 1) {
+                refs[c] = ~(int32_t)out.pairs.size();
+                out.pairs.push_back({items[cut[c]].t0, items[cut[c]].inst});
+            } else if (par > 0 && cut[c + 1] - cut[c] >= 4096) {
+                th.emplace_back([&, c] { node(cut[c], cut[c + 1], depth + 1, sub[c], par - 1); });
+            } else if (par > 0) {
+                node(cut[c], cut[c + 1], depth + 1, sub[c], 0);
+            } else {                                     // serial: the subtree follows in place
+                refs[c] = (int32_t)out.nodes.size();
+                node(cut[c], cut[c + 1], depth + 1, out, 0);
+            }
+        }
+        for (auto& t : th) t.join();
+        for (int c = 0; c < nc; ++c) {                   // append the subtrees in slot order
+            if (sub[c].nodes.empty()) continue;
+            const int32_t nb = (int32_t)out.nodes.size(), pb = (int32_t)out.pairs.size();
+            for (W4Node n : sub[c].nodes) {
+                for (int q = 0; q < 4; ++q) {
+                    if (!(n.pnear[0][q] < HUGE_VALF)) continue;   // empty slot
+                    n.ref[q] = n.ref[q] >= 0 ? n.ref[q] + nb : ~(~n.ref[q] + pb);
+                }
+                out.nodes.push_back(n);
+            }
+            out.pairs.insert(out.pairs.end(), sub[c].pairs.begin(), sub[c].pairs.end());
+            out.depth = std::max(out.depth, sub[c].depth);
+            refs[c] = nb;
+            FitOut().nodes.swap(sub[c].nodes);
+        }
+        W4Node& n = out.nodes[idx];
+        std::memset(&n, 0, sizeof(n));
+        for (int q = 0; q < 4; ++q) {
+            for (int y = 0; y < 3; ++y) {
+                n.pnear[y][q] = q < nc ? WideBuilder::down(blo[q][y]) : HUGE_VALF;
+                n.pfar[y][q] = q < nc ? WideBuilder::up(bhi[q][y]) : HUGE_VALF;
+            }
+            n.ref[q] = refs[q];
+        }
+    };
+    if (items.size() < 2) return;                        // one pair alone: tw_walk
+    FitOut out;
+    node(0, items.size(), 1, out, 2);
+    if (3 * out.depth + 2 > kStackCap) return;
+    const int64_t node_base = (int64_t)S.wnodes.size();
+    for (W4Node n : out.nodes) {                         // node refs relative to the whole array
+        for (int q = 0; q < 4; ++q)
+            if (n.pnear[0][q] < HUGE_VALF && n.ref[q] >= 0) n.ref[q] += (int32_t)node_base;
+        S.wnodes.push_back(n);
+    }
+    S.fpairs = std::move(out.pairs);
+    S.fit_root = (int32_t)node_base;
+    S.fit_nodes = (int64_t)out.nodes.size();
+    S.fit_depth = out.depth;
+    S.fit_coord = coord;
+    S.fit_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+}
+
 // Transformed scenes (instances with transforms; static, triangles only): the TLAS collapsed
 // into four-wide nodes whose terminal slots are instance markers carrying their TLAS leaf's box
 // (world space), and every BLAS collapsed on its own (local space; instances of one mesh share
@@ -710,6 +947,7 @@ static void build_wide(HostScene& S) {
 static void build_wide_tw(HostScene& S) {
     S.wnodes.clear(); S.lbox.clear(); S.winst.clear();
     S.wide_root = -1; S.wide_leaves = 0; S.wide_coord = 0.0; S.tw_tlas_nodes = 0;
+    S.fpairs.clear(); S.fit_root = -1; S.fit_nodes = 0; S.fit_depth = 0; S.fit_coord = 0.0;
     if (S.has_special || !S.has_tlas || S.max_motion != 0.0 || S.insts.empty()) return;
     for (const DInstance& I : S.insts)
         if (I.kind != kPrimTriangles) return;
@@ -765,6 +1003,11 @@ static void build_wide_tw(HostScene& S) {
     }
     for (const DWideInst& W : S.winst)
         if (!std::isfinite(W.bcoord)) { S.wnodes.clear(); S.lbox.clear(); S.winst.clear(); S.wide_root = -1; return; }
+    build_fit(S);
+    if (8 * S.wnodes.size() * sizeof(W4Node) >= (size_t(1) << 32)) {   // no room for the fit nodes
+        S.wnodes.resize(S.wnodes.size() - (size_t)S.fit_nodes);
+        S.fpairs.clear(); S.fit_root = -1; S.fit_nodes = 0;
+    }
     wide_octant_copies(S);
 }
 
@@ -1288,6 +1531,10 @@ int32_t build_host_scene(const rt_scene_desc* d, HostScene& S, std::string& err)
     }
     if (S.identity) build_wide(S);
     else build_wide_tw(S);
+    phase("wide");
+    if (trace && S.fit_root >= 0)
+        std::fprintf(stderr, "[build] fit: %zu pairs, %lld nodes, depth %lld, coord %.6g, %.1f ms\n", S.fpairs.size(),
+                     (long long)S.fit_nodes, (long long)S.fit_depth, S.fit_coord, S.fit_ms);
     if (S.recs.size() >= (size_t)INT32_MAX || S.tris.size() >= (size_t)INT32_MAX) { err = "scene too large for int32 refs"; return RT_ERR_UNSUPPORTED; }
     if (maxBlasDepth + 1 > 63 || tlasDepth + 1 > 63) {
         err = "BVH deeper than the reference's 64-entry stack (RTContext.swift:550, 623)";

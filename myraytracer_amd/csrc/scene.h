@@ -86,6 +86,13 @@ struct HostScene {
     // transformed scenes (static, triangles only): TLAS nodes first, then every BLAS's nodes
     std::vector<DWideInst> winst;          // per instance (layout.h DWideInst); empty: identity tree
     int64_t tw_tlas_nodes = 0;
+    // flattened instance tree (scene.cpp build_fit): world-space nodes over (leaf run, instance)
+    // pairs, appended to wnodes; fit_root < 0: none (tw_walk only)
+    std::vector<DFitPair> fpairs;
+    int32_t fit_root = -1;
+    int64_t fit_nodes = 0, fit_depth = 0;
+    double fit_coord = 0.0;                // bound on every magnitude the fit widening covers
+    double fit_ms = 0.0;                   // host time of build_fit
     // ---- bookkeeping / debug
     int64_t n_meshes = 0, n_tris = 0, n_spheres = 0, n_planes = 0;
     std::vector<uint64_t> inst_bvh_hash;   // per instance: canonical hash of its BLAS

@@ -205,93 +205,6 @@ __device__ __forceinline__ int tri_candidate(const Tri& T, const V3& o, const V3
     return t < ht ? 1 : (t == ht ? 2 : 0);
 }
 
-// Closest hit (SHADOW = false: h, tie) or any hit (SHADOW: returns occluded) of one ray.
-// COUNT: the work this walk executes (c.recs = four-wide nodes, c.tris = triangle tests) and its
-// per-iteration divergence (inner step / leaf run), as the binary walk's counters.
-template <bool COUNT, bool SHADOW>
-__device__ __forceinline__ bool wide_walk(const RenderParams& P, const V3& o, const V3& d, const V3& inv, double tlo,
-                                          double tmax, Hit& h, bool& tie, Stack& st, Counts& c) {
-    const WRay R = wide_ray(P, o, inv, P.wdelta);
-    const double eps = P.eps;
-    float lim = SHADOW ? wide_limit(P, tmax) : 3.0e38f;
-    const int base = st.sp;
-    int ref = P.wide_root;
-    bool occ = false;
-    const char* wbase = reinterpret_cast<const char*>(P.wnodes);
-    const auto* ctris = P.ctris;
-    const auto* tris = P.tris;
-    for (;;) {
-        if (COUNT) {
-            const bool in = ref >= 0;
-            const unsigned long long bi = __ballot(in), bl = __ballot(!in);
-            const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
-            c.it_wave_inner[SHADOW] += (first && bi) ? 1 : 0;
-            c.it_wave_leaf[SHADOW] += (first && bl) ? 1 : 0;
-            c.it_lane_inner[SHADOW] += in ? 1 : 0;
-            c.it_lane_leaf[SHADOW] += in ? 0 : 1;
-            if (SHADOW) c.it_shadow++; else c.it_closest++;
-            if (in) c.recs++;
-        }
-        if (ref >= 0) {
-            if (wide_inner(P, wbase, ref, R, lim, st)) continue;
-        } else {
-            const int t0 = ~ref;
-            int box = 0;                                   // leaf box: 0 unchecked, 1 passes, 2 fails
-            auto run = [&](const auto* tris) {
-                for (int t = t0;; ++t) {
-                    const auto T = tris[t];                // by value: `last` arrives with the vertices
-                    if (COUNT) c.tris++;
-                    if (SHADOW) {
-                        if (tri_shadow(T, o, d, 0.0, tmax, eps, P.fast_rcp)) {
-                            if (box == 0) box = leaf_box_exact(P, t0, o, d) ? 1 : 2;
-                            if (box == 1) return true;
-                        }
-                    } else {
-                        double tt, uu, vv;
-                        const int r = tri_candidate(T, o, d, tlo, eps, h.t, tt, uu, vv, P.fast_rcp);
-                        if (r != 0) {
-                            if (box == 0) box = leaf_box_exact(P, t0, o, d) ? 1 : 2;
-                            if (box == 1) {
-                                if (r == 1) {
-                                    h.t = tt; h.u = uu; h.v = vv; h.tri = t; h.inst = T.prim;
-                                    tie = false;
-                                    lim = wide_limit(P, tt);
-                                } else {
-                                    tie = true;
-                                }
-                            }
-                        }
-                    }
-                    if (T.last) break;
-                }
-                return false;
-            };
-            if (ctris ? run(ctris) : run(tris)) { occ = true; break; }
-        }
-        if (!wide_pop(st, base, lim, ref)) break;
-    }
-    st.reset(base);
-    return occ;
-}
-
-// ---- transformed scenes (static instances with transforms, triangles only; scene.cpp
-// build_wide_tw).  The reference walks the TLAS with the world ray and, at each TLAS leaf, every
-// instance's BLAS with that instance's local ray (RTContext.swift:619-720; the local direction is
-// not renormalised, so t is the same in both spaces).  A triangle is tested iff its TLAS leaf box
-// passes hitAABB with the world ray and its BLAS leaf box with the local ray (box nesting within
-// each tree, wide.h header).  This walk: the TLAS's four-wide nodes in world space (FP32,
-// widened by P.wdelta); a marker slot (its TLAS leaf's box) enters the instance with the exact
-// FP64 tests of the TLAS leaf box (world ray) and of the BLAS root box (local ray, :567-571) -
-// only instances the reference visits are entered - and continues with the BLAS's nodes and the
-// local ray, widened per ray by 2^-21 * max(|BLAS coordinate|, |local origin|) (the bound of the
-// wide.h header for this ray); candidates are accepted after the exact FP64 test of their leaf
-// box (local).  Stack entries above an instance's marker are its BLAS's, so popping a TLAS entry
-// (node < tw_tlas_nodes, or a marker) brings the world ray back.  Equal-t candidates (tie) and
-// lanes whose local 1/d leaves the FP32 range (redo) are re-walked in the reference's order
-// (device.h ut_walk) by the caller.
-__device__ __forceinline__ bool tw_is_tlas(const RenderParams& P, int ref) {
-    return ref >= 0 ? ref < P.tw_tlas_nodes : ~ref >= P.ut_marker_base;
-}
 // The world ray of a transformed walk: kept by the caller (TwWorld) or parked in this lane's
 // private memory (TwParked: read back only where the walk needs it - its start, an instance's
 // marker, the return to the TLAS - so it is not live, spilled, across the BLAS walks; the empty
@@ -315,6 +228,232 @@ struct TwParked {
     static constexpr bool kParked = true;
 };
 
+// ---- flattened instance tree (transformed scenes; scene.cpp build_fit, option fit).  One
+// world-space four-wide tree over every (instance, BLAS leaf run) pair: a pair's box is its local
+// leaf box through localToWorld (AABB.transformed, AABB.swift:71-92).  Why the walk returns the
+// reference's hit: the reference tests the triangles of leaf L of instance k iff hitAABB passes
+// for k's TLAS leaf box (world ray), k's BLAS root box and L's box (local ray: w2l applied to the
+// world ray in FP64, RTContext.swift:632-673, 567-571; ancestors pass by nesting, wide.h header),
+// and compares local t, which is world t (the local direction is not renormalised).  If the local
+// FP64 test of L passes, some t* >= eps puts the computed local ray within 2^-50 max(|box|, |o_l|)
+// of L per axis; through localToWorld (l2w w2l = I within kappa 2^-50, kappa = |l2w||w2l| <=
+// kFitKappa = 2^12, scene.cpp) the exact world ray at t* lies within ~2^-44 kappa R <= 2^-32 R
+// of the pair's box, R = fit_coord (every world/local magnitude and translation, scene.cpp) or
+// the ray origin's reach.  The render widens every box by wdelta = 2^-21 R (the FP32 bound of the
+// header) plus 2^-27 R (set_wide, fit scenes), so the walk enters every pair whose triangles the
+// reference tests, with the same pruning limits as the other walks (lim >= the current local t).
+// A candidate is accepted only after the exact FP64 tests of the three boxes, with the reference's
+// local ray (the same m4_point arithmetic as ut_walk); equal-t candidates raise `tie` and are
+// re-walked in the reference's order (ut_walk).  No local FP32 walk: local rays need no range.
+__device__ __forceinline__ bool fit_boxes_exact(const RenderParams& P, int k, int t0, const V3& o, const V3& d,
+                                                const V3& ol, const V3& dl) {
+    const DWideInst& WI = P.winst[k];
+    const DInstance& I = P.insts[k];
+    const double* b = P.lbox + 6 * (size_t)t0;
+    const V3 il = rcp(dl);
+    double tm;
+    return slab_hit<false>(b[0], b[1], b[2], b[3], b[4], b[5], ol, il, P.eps, tm) &&
+           slab_hit<false>(I.root_lo[0], I.root_lo[1], I.root_lo[2], I.root_hi[0], I.root_hi[1], I.root_hi[2], ol, il,
+                           P.eps, tm) &&
+           slab_hit<true>(WI.tbox[0], WI.tbox[1], WI.tbox[2], WI.tbox[3], WI.tbox[4], WI.tbox[5], o, rcp(d), P.eps, tm);
+}
+// instance k's local ray (ut_local's arithmetic for a static instance): worldToLocal through the
+// scalar cache when every active lane is in the same instance
+#ifndef MYRT_FIT_SCALAR
+#define MYRT_FIT_SCALAR 1   // worldToLocal through the scalar cache when uniform: 6,315 vs 6,237 Mrays/s without
+#endif
+#ifndef MYRT_FIT_CACHE
+#define MYRT_FIT_CACHE 1    // keep the last pair's local ray (its instance) across the walk: C3i 6,315 -> 6,567 Mrays/s (profiles/r06d_ab_c3i.txt)
+#endif
+__device__ __forceinline__ void fit_local(const RenderParams& P, int k, const V3& o, const V3& d, V3& ol, V3& dl) {
+    const int k0 = __builtin_amdgcn_readfirstlane(k);
+    if (MYRT_FIT_SCALAR && __all(k == k0)) {
+        const unsigned long long av = (unsigned long long)P.insts[k0].w2l;
+        const unsigned alo = __builtin_amdgcn_readfirstlane((unsigned)av);
+        const unsigned ahi = __builtin_amdgcn_readfirstlane((unsigned)(av >> 32));
+        typedef const __attribute__((address_space(4))) double c4_double;
+        c4_double* M = (c4_double*)((unsigned long long)alo | ((unsigned long long)ahi << 32));
+        double w[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) w[i] = M[(i / 3) * 4 + i % 3];
+        double m[16] = {w[0], w[1], w[2], 0.0, w[3], w[4], w[5], 0.0, w[6], w[7], w[8], 0.0, w[9], w[10], w[11], 1.0};
+        ol = m4_point(m, o, 1.0);
+        dl = m4_point(m, d, 0.0);
+        return;
+    }
+    const double* M = P.insts[k].w2l;
+    ol = m4_point(M, o, 1.0);
+    dl = m4_point(M, d, 0.0);
+}
+
+// Closest hit (SHADOW = false: h, tie) or any hit (SHADOW: returns occluded) of one ray.
+// COUNT: the work this walk executes (c.recs = four-wide nodes, c.tris = triangle tests) and its
+// per-iteration divergence (inner step / leaf run), as the binary walk's counters.
+// FIT: the flattened instance tree of a transformed scene (above): terminal slots are pairs.
+//
+// Postponed leaf runs (MYRT_POSTPONE = T > 0; Aila-Laine speculative traversal): a lane that
+// reaches a leaf run parks it and keeps stepping inner nodes (with its current, larger pruning
+// limit); the wave runs the parked leaf runs together once at least T lanes hold one, or when
+// no lane can take an inner step (its stack is empty, or it holds a parked run and has met a
+// second).  Only the order in which leaf runs are tested changes, and with it only which of
+// several EQUAL-t candidates is met first - those lanes raise `tie` whatever the order and are
+// re-walked in the reference's order - while the pruning limit stays >= the current hit's t at
+// every test, so no leaf whose box holds the final hit is pruned: the header's argument holds.
+#ifndef MYRT_POSTPONE
+#define MYRT_POSTPONE 0
+#endif
+// W: the ray, kept by the caller (TwWorld) or parked (fit walks of the megakernels: the world ray
+// is read back at a pair, where its local ray is formed, and not live across the walk).
+template <bool COUNT, bool SHADOW, bool FIT = false, class World = TwWorld>
+__device__ __forceinline__ bool wide_walk(const RenderParams& P, const World& W, const V3& inv, double tlo,
+                                          double tmax, Hit& h, bool& tie, Stack& st, Counts& c) {
+    const WRay R = wide_ray(P, W.o(), inv, P.wdelta);
+    const double eps = P.eps;
+    float lim = SHADOW ? wide_limit(P, tmax) : 3.0e38f;
+    const int base = st.sp;
+    int ref = FIT ? P.fit_root : P.wide_root;
+    bool occ = false;
+    const char* wbase = reinterpret_cast<const char*>(P.wnodes);
+    const auto* ctris = P.ctris;
+    const auto* tris = P.tris;
+    // the terminal slot ~x: the leaf run starting at TriRec x, or (FIT) pair x; true = occluded
+#if MYRT_FIT_CACHE
+    int ck = -1;                                           // FIT: the instance of the local ray in cro/crd
+    V3 cro = v3(0, 0, 0), crd = v3(0, 0, 0);
+#endif
+    auto leaf = [&](const int x) -> bool {
+        int t0 = x, k = 0;
+        V3 ro, rd;                                         // the ray the triangles are tested with
+        if (FIT) {
+            const DFitPair pr = P.fpairs[x];
+            t0 = pr.t0;
+            k = pr.inst;
+#if MYRT_FIT_CACHE
+            if (k != ck) {
+                fit_local(P, k, W.o(), W.d(), cro, crd);
+                ck = k;
+            }
+            ro = cro;
+            rd = crd;
+#else
+            fit_local(P, k, W.o(), W.d(), ro, rd);
+#endif
+        } else {
+            ro = W.o();
+            rd = W.d();
+        }
+        int box = 0;                                       // leaf box: 0 unchecked, 1 passes, 2 fails
+        auto exact = [&]() {
+            return FIT ? fit_boxes_exact(P, k, t0, W.o(), W.d(), ro, rd) : leaf_box_exact(P, t0, ro, rd);
+        };
+        auto run = [&](const auto* tris) {
+            for (int t = t0;; ++t) {
+                const auto T = tris[t];                    // by value: `last` arrives with the vertices
+                if (COUNT) c.tris++;
+                if (SHADOW) {
+                    if (tri_shadow(T, ro, rd, 0.0, tmax, eps, P.fast_rcp)) {
+                        if (box == 0) box = exact() ? 1 : 2;
+                        if (box == 1) return true;
+                    }
+                } else {
+                    double tt, uu, vv;
+                    const int r = tri_candidate(T, ro, rd, tlo, eps, h.t, tt, uu, vv, P.fast_rcp);
+                    if (r != 0) {
+                        if (box == 0) box = exact() ? 1 : 2;
+                        if (box == 1) {
+                            if (r == 1) {
+                                h.t = tt; h.u = uu; h.v = vv; h.tri = t; h.inst = FIT ? k : T.prim;
+                                tie = false;
+                                lim = wide_limit(P, tt);
+                            } else {
+                                tie = true;
+                            }
+                        }
+                    }
+                }
+                if (T.last) break;
+            }
+            return false;
+        };
+        return ctris ? run(ctris) : run(tris);
+    };
+#if MYRT_POSTPONE
+    bool live = true;                                      // ref holds a node or a leaf run to visit
+    int pend = 0;                                          // the parked leaf run (a negative ref)
+    bool hasp = false;
+    for (;;) {
+        const bool step = live && ref >= 0;
+        if (COUNT) {
+            const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
+            c.it_wave_inner[SHADOW] += (first && __ballot(step)) ? 1 : 0;
+            c.it_lane_inner[SHADOW] += step ? 1 : 0;
+            if (SHADOW) c.it_shadow++; else c.it_closest++;
+            if (step) c.recs++;
+        }
+        if (step) {
+            if (!wide_inner(P, wbase, ref, R, lim, st)) live = wide_pop(st, base, lim, ref);
+        } else if (live && !hasp) {
+            pend = ref;
+            hasp = true;
+            live = wide_pop(st, base, lim, ref);
+        }
+        if (__popcll(__ballot(hasp)) >= MYRT_POSTPONE || !__any(live && (ref >= 0 || !hasp))) {
+            if (COUNT) {
+                const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
+                c.it_wave_leaf[SHADOW] += (first && __ballot(hasp)) ? 1 : 0;
+                c.it_lane_leaf[SHADOW] += hasp ? 1 : 0;
+            }
+            if (hasp) {
+                hasp = false;
+                if (leaf(~pend)) { occ = true; live = false; }
+            }
+        }
+        if (!__any(live || hasp)) break;
+    }
+#else
+    for (;;) {
+        if (COUNT) {
+            const bool in = ref >= 0;
+            const unsigned long long bi = __ballot(in), bl = __ballot(!in);
+            const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
+            c.it_wave_inner[SHADOW] += (first && bi) ? 1 : 0;
+            c.it_wave_leaf[SHADOW] += (first && bl) ? 1 : 0;
+            c.it_lane_inner[SHADOW] += in ? 1 : 0;
+            c.it_lane_leaf[SHADOW] += in ? 0 : 1;
+            if (SHADOW) c.it_shadow++; else c.it_closest++;
+            if (in) c.recs++;
+        }
+        if (ref >= 0) {
+            if (wide_inner(P, wbase, ref, R, lim, st)) continue;
+        } else if (leaf(~ref)) {
+            occ = true;
+            break;
+        }
+        if (!wide_pop(st, base, lim, ref)) break;
+    }
+#endif
+    st.reset(base);
+    return occ;
+}
+
+// ---- transformed scenes (static instances with transforms, triangles only; scene.cpp
+// build_wide_tw).  The reference walks the TLAS with the world ray and, at each TLAS leaf, every
+// instance's BLAS with that instance's local ray (RTContext.swift:619-720; the local direction is
+// not renormalised, so t is the same in both spaces).  A triangle is tested iff its TLAS leaf box
+// passes hitAABB with the world ray and its BLAS leaf box with the local ray (box nesting within
+// each tree, wide.h header).  This walk: the TLAS's four-wide nodes in world space (FP32,
+// widened by P.wdelta); a marker slot (its TLAS leaf's box) enters the instance with the exact
+// FP64 tests of the TLAS leaf box (world ray) and of the BLAS root box (local ray, :567-571) -
+// only instances the reference visits are entered - and continues with the BLAS's nodes and the
+// local ray, widened per ray by 2^-21 * max(|BLAS coordinate|, |local origin|) (the bound of the
+// wide.h header for this ray); candidates are accepted after the exact FP64 test of their leaf
+// box (local).  Stack entries above an instance's marker are its BLAS's, so popping a TLAS entry
+// (node < tw_tlas_nodes, or a marker) brings the world ray back.  Equal-t candidates (tie) and
+// lanes whose local 1/d leaves the FP32 range (redo) are re-walked in the reference's order
+// (device.h ut_walk) by the caller.
+__device__ __forceinline__ bool tw_is_tlas(const RenderParams& P, int ref) {
+    return ref >= 0 ? ref < P.tw_tlas_nodes : ~ref >= P.ut_marker_base;
+}
 template <bool SHADOW, class World>
 __device__ __forceinline__ bool tw_walk(const RenderParams& P, const World& W, double tlo, double tmax,
                                         Hit& h, bool& tie, bool& redo, Stack& st) {

@@ -246,20 +246,22 @@ def test_bench_strong_split_eight_ranks_on_one_gpu():
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("name", ["c3i", "c3g", "c3d", "c3r"])
+@pytest.mark.parametrize("name", ["c3i", "c3i_tw", "c3g", "c3d", "c3r"])
 def test_general_path_bench_configs_full_frame(scene_dir, name):
     """The bench's general-path configs on full 1920x1080 frames against the oracle: C3i (C3's
     geometry as 25 transformed mesh instances: the literal TLAS->BLAS walk, RTContext.swift:
-    619-720) and C3g (glass spheres + two area lights: render_full with k_events/k_jscan,
+    619-720; the flattened instance tree, and tw_walk with option fit = 0) and C3g (glass spheres + two area lights: render_full with k_events/k_jscan,
     Object+Extension.swift:145-251) and C3d (the glass spheres with the point light only: level
     passes + node shading without events), through bench.py's call (RGBA8 into page-locked
     memory) and the FP64 frame."""
-    make = {"c3i": scenes.scene_c3_instanced, "c3g": scenes.scene_c3_glass,
+    make = {"c3i": scenes.scene_c3_instanced, "c3i_tw": scenes.scene_c3_instanced, "c3g": scenes.scene_c3_glass,
             "c3r": lambda path_dir: scenes.scene_c3_glass(path_dir=path_dir, rough=True),
             "c3d": lambda path_dir: scenes.scene_c3_glass(path_dir=path_dir, area_lights=False)}[name]
     sc = make(path_dir=scene_dir)
     ref, ref8, ost = oracle.OracleScene(_inline(sc)).render(0, threads=0, rgba=True)
     eng = M.RayTracerEngine(sc)
+    if name == "c3i_tw":
+        eng.set_option("fit", 0)
     H, W = ref.shape[:2]
     rgba = M.pinned_array((H, W, 4), np.uint8)
     rgba.fill(0)

@@ -25,7 +25,8 @@ pytestmark = pytest.mark.gpu
 # walk name -> render options (identity scenes: wide / unified / general; instanced scenes:
 # transformed / general)
 WALKS = {"wide": {}, "unified": {"wide": 0}, "general": {"unified": 0},
-         "transformed": {}, "transformed_binary": {"wide": 0}, "nested": {"unified_transformed": 0}}
+         "transformed": {}, "transformed_tw": {"fit": 0}, "transformed_binary": {"wide": 0},
+         "nested": {"unified_transformed": 0}}
 
 
 def _engine(sc, walk):
@@ -295,19 +296,20 @@ def _transformed_instances():
     return sc
 
 
-@pytest.mark.parametrize("walk", ["transformed", "transformed_binary", "nested"])
+@pytest.mark.parametrize("walk", ["transformed", "transformed_tw", "transformed_binary", "nested"])
 def test_transformed_mesh_instances(walk):
-    """Rotated / scaled / translated mesh instances: the four-wide transformed walk (wide.h
-    tw_walk, the default), the unified transformed walk (device.h ut_walk, option wide = 0) and
-    the nested walk give the oracle's intersectTLAS / occludedTLAS bit for bit - including
-    axis-aligned and signed-zero directions in local space."""
+    """Rotated / scaled / translated mesh instances: the flattened instance tree (wide.h
+    fit_walk, the default), the four-wide transformed walk (tw_walk, option fit = 0), the unified
+    transformed walk (device.h ut_walk, option wide = 0) and the nested walk give the oracle's
+    intersectTLAS / occludedTLAS bit for bit - including axis-aligned and signed-zero directions
+    in local space."""
     sc = _transformed_instances()
     O, D = _ray_set(np.array([0.0, 0.0, 0.0]), 4.0, 3000, 23)
     _check_closest(sc, O, D, walk=walk)
     _check_occluded(sc, O, D, np.random.RandomState(6).uniform(0.1, 8.0, size=len(O)), walk=walk)
 
 
-@pytest.mark.parametrize("walk", ["transformed", "transformed_binary", "nested"])
+@pytest.mark.parametrize("walk", ["transformed", "transformed_tw", "transformed_binary", "nested"])
 def test_equal_t_ties_between_transformed_instances(walk):
     """Two instances of one mesh under the same rotation and scale, with different materials:
     every hit is a tie between them, and the walks must return the reference's instance (the
@@ -341,7 +343,7 @@ def test_equal_t_ties_between_transformed_instances(walk):
     ref, ref8, _ = oracle.OracleScene(sc).render(0, 0, 1, threads=0, rgba=True)
     eng.close()
     assert float(np.abs(rgb - ref).max()) <= 1e-5 and np.array_equal(rgba, ref8)
-    if walk == "transformed":                        # four-wide (wide.h tw_walk): ties re-walked
+    if walk in ("transformed", "transformed_tw"):    # four-wide (fit_walk / tw_walk): ties re-walked
         assert st.rewalked > 0
     else:                                            # the binary walks keep the reference order
         assert st.rewalked == 0

@@ -56,17 +56,19 @@ def _far(sc, scale, offset):
     return s
 
 
-def _engine(sc, permille=None):
+def _engine(sc, permille=None, fit=None):
     eng = M.RayTracerEngine(sc)
     if permille is not None:
         eng.set_unsafe_option("wide_delta_scale", permille)
+    if fit is not None:
+        eng.set_option("fit", fit)
     assert eng.get_option("wide") == 1
     return eng
 
 
-def _closest_mismatch(sc, O, D, permille=None, orc=None):
+def _closest_mismatch(sc, O, D, permille=None, orc=None, fit=None):
     """Rays whose closest hit (t, point, normal, material) differs from the oracle's."""
-    eng = _engine(sc, permille)
+    eng = _engine(sc, permille, fit)
     tg, pg, ng, mg = eng.trace_rays(O, D)
     eng.close()
     to, po, no, mo = (orc or oracle.OracleScene(sc)).trace_rays(O, D)
@@ -76,8 +78,8 @@ def _closest_mismatch(sc, O, D, permille=None, orc=None):
     return bad, np.isfinite(to)
 
 
-def _occluded_mismatch(sc, O, D, tmax, permille=None, orc=None):
-    eng = _engine(sc, permille)
+def _occluded_mismatch(sc, O, D, tmax, permille=None, orc=None, fit=None):
+    eng = _engine(sc, permille, fit)
     g = eng.occluded_rays(O, D, tmax)
     eng.close()
     o = (orc or oracle.OracleScene(sc)).occluded_rays(O, D, tmax)
@@ -316,10 +318,12 @@ def _far_instances():
     return sc, mats, centre
 
 
-def test_transformed_instances_far_away_and_teeth():
+@pytest.mark.parametrize("fit", [1, 0])
+def test_transformed_instances_far_away_and_teeth(fit):
     """Near-vertex rays at instances of a far mesh (world and local coordinates ~1e6): bit-exact
-    closest hits and occlusion through the four-wide transformed walk, and the frame; without the
-    widening (wide_delta_scale = 0, world and local) the same rays differ from the oracle."""
+    closest hits and occlusion through the flattened instance tree (fit = 1, wide.h fit_walk) and
+    the four-wide transformed walk (fit = 0, tw_walk), and the frame; without the widening
+    (wide_delta_scale = 0, world and local) the same rays differ from the oracle."""
     sc, mats, centre = _far_instances()
     mesh = sc.objects[0]
     P, F = np.asarray(mesh.positions), np.asarray(mesh.indices)
@@ -331,18 +335,52 @@ def test_transformed_instances_far_away_and_teeth():
         Os.append(O); Ds.append(D)
     O, D = np.concatenate(Os), np.concatenate(Ds)
     orc = oracle.OracleScene(sc)
-    bad, hit = _closest_mismatch(sc, O, D, orc=orc)
+    bad, hit = _closest_mismatch(sc, O, D, orc=orc, fit=fit)
     assert not bad.any(), f"{int(bad.sum())} of {len(O)} closest hits differ"
     assert hit.mean() > 0.3
     t, *_ = orc.trace_rays(O, D)
     tmax = np.where(np.isfinite(t), t * (1 + rng.choice([-1e-9, 1e-9], size=len(t))), 1e7)
-    bado, occ = _occluded_mismatch(sc, O, D, tmax, orc=orc)
+    bado, occ = _occluded_mismatch(sc, O, D, tmax, orc=orc, fit=fit)
     assert not bado.any()
-    eng = _engine(sc)
+    eng = _engine(sc, fit=fit)
     rgb, rgba, st = eng.render_rows(0, 0, 1, True)
     eng.close()
     ref, ref8, _ = orc.render(0, 0, 1, threads=0, rgba=True)
     assert float(np.abs(rgb - ref).max()) <= TOL and np.array_equal(rgba, ref8)
+    bad0, _ = _closest_mismatch(sc, O, D, permille=0, orc=orc, fit=fit)
+    print(f"transformed (fit = {fit}), no widening: {int(bad0.sum())} / {len(O)} closest hits differ")
+    # tw_walk's local FP32 boxes are tight: the set reaches their bound.  The flattened tree's world
+    # boxes of ROTATED instances are loose (AABB.transformed of a rotated leaf box), so the set
+    # cannot: its teeth are test_fit_tree_reaches_the_bound (translated instances, tight boxes).
+    if not fit:
+        assert bad0.any(), "no mismatch without widening: the set does not reach the bound"
+
+
+def test_fit_tree_reaches_the_bound():
+    """The flattened instance tree at its edge: C2's mesh at 1e6 as a TRANSLATED instance (local
+    coordinates = the far geometry minus the offset, exactly; the pair boxes equal the identity
+    scene's leaf boxes), near-vertex rays bit-exact (closest + any hit) at the production widening,
+    and mismatches without it - so wide.h fit_walk's widening is what keeps them exact."""
+    sc, scale, off = _far_c2("1e6")
+    mesh = sc.objects[0]
+    Pw = np.asarray(mesh.positions)
+    F = np.asarray(mesh.indices)
+    mesh.positions = Pw - off                             # exact: multiples of 2^-4 below 2^15
+    assert np.array_equal(mesh.positions + off, Pw)
+    M4 = np.eye(4)
+    M4[:3, 3] = off
+    mesh.transform = tuple(M4.T.reshape(-1))
+    rng = np.random.RandomState(61)
+    O, D = _near_vertex_rays(Pw, F, 12000, rng, 3.0 * scale)
+    orc = oracle.OracleScene(sc)
+    bad, hit = _closest_mismatch(sc, O, D, orc=orc)
+    assert not bad.any(), f"{int(bad.sum())} of {len(O)} closest hits differ"
+    assert hit.mean() > 0.3
+    t, *_ = orc.trace_rays(O, D)
+    tmax = np.where(np.isfinite(t), t * (1 + rng.choice([-1e-9, 1e-9], size=len(t))), 1e3 * scale)
+    bado, _ = _occluded_mismatch(sc, O, D, tmax, orc=orc)
+    assert not bado.any()
     bad0, _ = _closest_mismatch(sc, O, D, permille=0, orc=orc)
-    print(f"transformed, no widening: {int(bad0.sum())} / {len(O)} closest hits differ")
-    assert bad0.any(), "no mismatch without widening: the set does not reach the bound"
+    bad0t, _ = _closest_mismatch(sc, O, D, permille=0, orc=orc, fit=0)
+    print(f"translated instance, no widening: fit {int(bad0.sum())} / {len(O)}, tw {int(bad0t.sum())} closest hits differ")
+    assert bad0.any(), "no mismatch without widening: the set does not reach the fit tree's bound"
