@@ -293,7 +293,11 @@ constexpr int kCounterWords = 64;   // u64 words behind RenderParams::counters
 // kQHdrCnt the (level, region) counters, 128 B apart; k_queue_done zeroes the counters after
 // the last level.
 constexpr int kMaxQueueLevels = 15;
-constexpr int kQRegions = 32;
+#ifndef MYRT_QREGION_BITS
+#define MYRT_QREGION_BITS 5
+#endif
+constexpr int kQRegionBits = MYRT_QREGION_BITS;    // <= 6: k_bounce holds one region per lane
+constexpr int kQRegions = 1 << kQRegionBits;
 constexpr int kQHdrCap = 16, kQHdrCnt = 64, kQCntStride = 16;
 constexpr int kQHdrWords = kQHdrCnt + kMaxQueueLevels * kQRegions * kQCntStride;
 constexpr int kCounterShadowTraced = 13;

@@ -400,6 +400,9 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
                          Counts& c, bool park_rng, int i0 = 0, int j0 = 0,
                          bool* deferred = nullptr, int qregion = 0) {
     static_assert(!(QUEUE && BOUNCE), "the queued primary pass has no bounce loop");
+    // flattened-tree scenes are static (scene.cpp build_wide_tw): motion * time == 0 for every time in
+    // [0, 1), so the ray time need not stay live (the caller still draws it: the PCG32 sequence)
+    if (WALK == kWalkFit) time = 0.0;
     auto park = [&]() { if (BOUNCE && park_rng) *pix_slot(3) = __builtin_bit_cast(double, rng.state); };
     auto unpark = [&]() {
         if (BOUNCE && park_rng) {
@@ -746,8 +749,8 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long x
 // wave w of the grid takes the batches of 64 consecutive records w, w + G, ... of the level's
 // regions laid end to end (lane r < kQRegions holds region r's count, clamped to the capacity,
 // and the exclusive prefix).  A mirror/conductor hit below maxRecursionDepth reserves a
-// level + 1 record (q_reserve, region = the batch number mod kQRegions: a region takes at most
-// ceil(batches / kQRegions) batches), writes its reflected ray there with this record as the
+// level + 1 record (q_reserve, in its own record's region: a region holds at most the rays of
+// ceil(tiles / kQRegions) primary-pass tiles), writes its reflected ray there with this record as the
 // parent, and its own Lo after the shadow walks; any other end resolves the sample backward
 // along the parents and stores the pixel.
 #ifndef MYRT_QUEUE_WPE
@@ -776,7 +779,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
         const unsigned b = x0 + (unsigned)lane;          // this lane's ray
         int jl = 0, jh = kQRegions;                      // its region: the last one with ex <= b
 #pragma unroll
-        for (int s = 0; s < 5; ++s) {
+        for (int s = 0; s < kQRegionBits; ++s) {
             const int mid = (jl + jh) >> 1;
             if ((unsigned)__shfl((int)ex, mid, 64) <= b) jl = mid; else jh = mid;
         }
@@ -785,7 +788,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
         if (b >= T) continue;
         const BounceRec& R = P.bounce[g];
         const V3 o = ld3(R.o), d = ld3(R.d);
-        const double time = WALK == kWalkIdentity ? 0.0 : R.time;
+        const double time = (WALK == kWalkIdentity || WALK == kWalkFit) ? 0.0 : R.time;
         V3 L = v3(0, 0, 0);
         bool hit = false, want = false, computeDirect = false;
         V3 p, N, Lo;
@@ -809,17 +812,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
                 want = (Mp->type == RT_MAT_MIRROR || Mp->type == RT_MAT_CONDUCTOR) && level < P.max_depth;
             }
         }
-        const unsigned long long m = __ballot(want);
+        // The next level's records go to this record's own region (jl): a region's rays at every
+        // level are then the descendants of a fixed set of primary-pass waves, so its count is the
+        // same every frame (with the batch's region it varied with the atomics' order, and the
+        // by-need arenas kept growing - a hipMalloc inside the pipelined loop).  One atomic per
+        // region the wave's reflecting lanes are in (one, at most a few at sparse levels).
+        unsigned long long pend = __ballot(want);
         long long q = -1;
-        if (m) {                                         // the records, formed while the atomic returns
-            const int region = (int)((x0 >> 6) % kQRegions);
-            const QTicket tk = q_issue(P, level + 1, region, m);
+        if (pend) {
             QRay qr{};
             if (want) {
                 PCG32 r = PCG32::resume(R.rng, pixel_seed(R.i, R.j));
                 qr = queue_ray(P, *Mp, d, N, p, r);
             }
-            q = q_index(P, level + 1, region, m, want, tk);
+            while (pend) {
+                const int r0 = __shfl(jl, __builtin_ctzll(pend), 64);
+                const bool mine = want && jl == r0;
+                const unsigned long long m = __ballot(mine);
+                const QTicket tk = q_issue(P, level + 1, r0, m);
+                const long long qq = q_index(P, level + 1, r0, m, mine, tk);
+                if (mine) q = qq;
+                pend &= ~m;
+            }
             if (q >= 0) queue_store(P, q, qr, R.time, R.i, R.j, g);
         }
         if (hit) {

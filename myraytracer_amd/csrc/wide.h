@@ -317,10 +317,10 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const World& W,
     const auto* ctris = P.ctris;
     const auto* tris = P.tris;
     // the terminal slot ~x: the leaf run starting at TriRec x, or (FIT) pair x; true = occluded
-#if MYRT_FIT_CACHE
-    int ck = -1;                                           // FIT: the instance of the local ray in cro/crd
+    // FIT: the instance of the local ray kept in cro/crd (MYRT_FIT_CACHE: 1 = every walk, 2 = closest hit)
+    constexpr bool kCache = MYRT_FIT_CACHE == 1 || (MYRT_FIT_CACHE == 2 && !SHADOW);
+    int ck = -1;
     V3 cro = v3(0, 0, 0), crd = v3(0, 0, 0);
-#endif
     auto leaf = [&](const int x) -> bool {
         int t0 = x, k = 0;
         V3 ro, rd;                                         // the ray the triangles are tested with
@@ -328,16 +328,16 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const World& W,
             const DFitPair pr = P.fpairs[x];
             t0 = pr.t0;
             k = pr.inst;
-#if MYRT_FIT_CACHE
-            if (k != ck) {
-                fit_local(P, k, W.o(), W.d(), cro, crd);
-                ck = k;
+            if (kCache) {
+                if (k != ck) {
+                    fit_local(P, k, W.o(), W.d(), cro, crd);
+                    ck = k;
+                }
+                ro = cro;
+                rd = crd;
+            } else {
+                fit_local(P, k, W.o(), W.d(), ro, rd);
             }
-            ro = cro;
-            rd = crd;
-#else
-            fit_local(P, k, W.o(), W.d(), ro, rd);
-#endif
         } else {
             ro = W.o();
             rd = W.d();
