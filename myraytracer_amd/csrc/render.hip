@@ -532,12 +532,16 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
 #define MYRT_QPRIM_WPE 4    // the queued primary pass of the compacted bounce render
 #endif
 #ifndef MYRT_TW_WPE
-#define MYRT_TW_WPE 4       // the transformed-walk primary instantiation (C3i)
+#define MYRT_TW_WPE 4       // the transformed-walk primary instantiation (C3i, option fit = 0)
+#endif
+#ifndef MYRT_FIT_WPE
+#define MYRT_FIT_WPE 4      // the flattened-instance-tree primary instantiation (C3i)
 #endif
 #if MYRT_MEGA_WPE > 0
 #define MYRT_MEGA_ATTR \
     __attribute__((amdgpu_waves_per_eu(BOUNCE ? MYRT_BOUNCE_WPE : QUEUE ? MYRT_QPRIM_WPE : \
-                                       WALK == kWalkTransformed ? MYRT_TW_WPE : MYRT_MEGA_WPE)))
+                                       WALK == kWalkTransformed ? MYRT_TW_WPE : WALK == kWalkFit ? MYRT_FIT_WPE : \
+                                       MYRT_MEGA_WPE)))
 #else
 #define MYRT_MEGA_ATTR
 #endif

@@ -79,7 +79,13 @@ def kernel_total_ms(path, kernel):
 
 def chain(a):
     """Per-frame figures of a multi-kernel frame (see the module docstring)."""
-    ks = a.kernel
+    def present(k):
+        try:
+            kernel_total_ms(a.trace, k)
+            return True
+        except SystemExit:
+            return False
+    ks = [a.kernel[0]] + [k for k in a.kernel[1:] if present(k)]   # a config may skip some passes
     _, frames = kernel_total_ms(a.trace, ks[0])
     _, pmc_frames = counter_total(a.fetch, "FETCH_SIZE", ks[0])
 

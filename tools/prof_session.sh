@@ -12,8 +12,12 @@ KX=""
 case " $* " in
   *" --config c5 "*) K="${KERNEL:-render_kernel<false, false, 1, true>}"
                      KX="--kernel 'k_bounce<1>' --kernel k_queue_done" ;;
-  *" --config c3i "*) K="${KERNEL:-render_kernel<false, false, 2, false>}" ;;
-  *" --config c3g "*|*" --config c3r "*) K="${KERNEL:-render_full<false, false, 1>}" ;;
+  *" --config c3i "*) K="${KERNEL:-render_kernel<false, false, 3, false>}" ;;
+  # full trace() frames (C3g / C3d: level passes; C3r: depth-first k_events): the frame chain
+  *" --config c3g "*|*" --config c3d "*) K="${KERNEL:-k_level<1>}"
+      KX="--kernel 'k_level_c<1>' --kernel k_ccount --kernel k_clist --kernel k_jofs --kernel k_jscan --kernel 'k_shade_c<1>' --kernel 'render_full<false, false, 1>'" ;;
+  *" --config c3r "*) K="${KERNEL:-k_events<false, 1>}"
+      KX="--kernel k_jscan --kernel k_ccount --kernel k_clist --kernel 'k_shade_c<1>' --kernel 'render_full<false, false, 1>'" ;;
   *) K="${KERNEL:-render_kernel<false, false, 1, false>}" ;;
 esac
 steps=(
