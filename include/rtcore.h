@@ -373,6 +373,10 @@ uint64_t rt_debug_bvh_hash(const rt_scene* scene, int32_t instance);
 /* Host-only build (no device): hashes[0..n) per instance, hashes[n] = TLAS. */
 int32_t  rt_debug_host_build(const rt_scene_desc* desc, uint64_t* hashes, int32_t max_hashes,
                              int32_t* n_instances, rt_scene_info* info);
+/* Host-only build of a transformed scene's flattened instance tree (wide.h fit_walk): out[0] =
+ * pairs (0: no tree), out[1] = nodes, out[2] = depth, out[3] = leaf runs over all instances,
+ * out[4] = a hash of the pairs and the nodes (octant copy 0). */
+int32_t  rt_debug_fit_build(const rt_scene_desc* desc, int64_t* out);
 
 /* Explicit-ray queries on device `slot` through the render kernels' traversal (host
  * arrays, n rays; o/d: 3 doubles per ray).  rt_debug_trace_rays = intersectTLAS

@@ -125,7 +125,7 @@ RT_OBJ_MESH, RT_OBJ_TRIANGLE, RT_OBJ_SPHERE, RT_OBJ_PLANE, RT_OBJ_MESH_INSTANCE 
 EXPORTED_SYMBOLS = [
     "rt_scene_create", "rt_scene_destroy", "rt_scene_info_get", "rt_render", "rt_render_device",
     "rt_stats_collect", "rt_rows_for_chunks", "rt_render_device_counted", "rt_last_error", "rt_version",
-    "rt_ply_load", "rt_ply_free", "rt_debug_bvh_hash", "rt_debug_host_build",
+    "rt_ply_load", "rt_ply_free", "rt_debug_bvh_hash", "rt_debug_host_build", "rt_debug_fit_build",
     "rt_debug_trace_rays", "rt_debug_occluded_rays", "rt_host_alloc", "rt_host_free", "rt_debug_wave_times",
     "rt_debug_rcp", "rt_render_submit", "rt_render_wait",
     "rt_render_ex", "rt_host_register", "rt_host_unregister",
@@ -203,6 +203,9 @@ def bind(lib: C.CDLL) -> C.CDLL:
     lib.rt_debug_bvh_hash.restype = C.c_uint64
     lib.rt_debug_host_build.argtypes = [P(rt_scene_desc), P(C.c_uint64), C.c_int32, c_int32_p, P(rt_scene_info)]
     lib.rt_debug_host_build.restype = C.c_int32
+    if hasattr(lib, "rt_debug_fit_build"):   # round 6 (an older build may be loaded for an A/B, MYRT_LIB)
+        lib.rt_debug_fit_build.argtypes = [P(rt_scene_desc), P(C.c_int64)]
+        lib.rt_debug_fit_build.restype = C.c_int32
     lib.rt_debug_trace_rays.argtypes = [C.c_void_p, C.c_int32, C.c_int32, c_double_p, c_double_p, c_double_p,
                                         c_double_p, c_double_p, c_double_p, c_double_p, c_int32_p]
     lib.rt_debug_trace_rays.restype = C.c_int32

@@ -3074,6 +3074,48 @@ int32_t rt_debug_host_build(const rt_scene_desc* desc, uint64_t* hashes, int32_t
     }
 }
 
+int32_t rt_debug_fit_build(const rt_scene_desc* desc, int64_t* out) {
+    if (!desc) return fail(RT_ERR_NO_SCENE, "No scene loaded.");
+    if (!out) return fail(RT_ERR_INVALID_ARG, "NULL argument");
+    try {
+        HostScene S;
+        std::string err;
+        const int32_t rc = build_host_scene(desc, S, err);
+        if (rc != RT_OK) return fail(rc, err);
+        for (int k = 0; k < 5; ++k) out[k] = 0;
+        int64_t runs = 0;                       // leaf runs over all instances (the pairs the tree must hold)
+        for (const DInstance& I : S.insts) {
+            if (I.kind != kPrimTriangles) continue;
+            if (I.root_ref < 0) { ++runs; continue; }
+            std::vector<int32_t> st{I.root_ref};
+            while (!st.empty()) {
+                const WRec& r = S.recs[st.back()];
+                st.pop_back();
+                for (int c = 0; c < 2; ++c) {
+                    if (r.ref[c] < 0) ++runs;
+                    else st.push_back(r.ref[c]);
+                }
+            }
+        }
+        out[3] = runs;
+        if (S.fit_root < 0) return RT_OK;
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](const void* p, size_t n) {
+            const unsigned char* b = static_cast<const unsigned char*>(p);
+            for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
+        };
+        mix(S.fpairs.data(), S.fpairs.size() * sizeof(DFitPair));
+        mix(&S.wnodes[(size_t)S.fit_root], (size_t)S.fit_nodes * sizeof(W4Node));
+        out[0] = (int64_t)S.fpairs.size();
+        out[1] = S.fit_nodes;
+        out[2] = S.fit_depth;
+        out[4] = (int64_t)(h >> 1);
+        return RT_OK;
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_INVALID_ARG, e.what());
+    }
+}
+
 // ---- debug: explicit rays through the render kernels' traversal
 static int32_t debug_rays(rt_scene* s, int32_t slot, int32_t n, const double* o, const double* d, const double* tl,
                           const double* time, double* out_t, double* out_p, double* out_n, int32_t* out_mat,

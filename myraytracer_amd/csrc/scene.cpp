@@ -922,7 +922,89 @@ static void build_fit(HostScene& S) {
     };
     if (items.size() < 2) return;                        // one pair alone: tw_walk
     FitOut out;
-    node(0, items.size(), 1, out, 2);
+#ifndef MYRT_FIT_BUILD
+#define MYRT_FIT_BUILD 1
+#endif
+    if (MYRT_FIT_BUILD == 0) {
+        node(0, items.size(), 1, out, 2);
+    } else {
+        // The reference's binned SAH builder (build_ref_bvh, BVH.swift:128-250) over the pairs'
+        // world boxes, collapsed to four-wide nodes as build_wide collapses C3's tree: a node opens
+        // its largest child while the children fit four slots; every pair is one terminal slot.
+        PrimSet ps;
+        ps.n = (int64_t)items.size();
+        ps.bmin.resize(3 * items.size()); ps.bmax.resize(3 * items.size()); ps.cen.resize(3 * items.size());
+        for (size_t i = 0; i < items.size(); ++i)
+            for (int y = 0; y < 3; ++y) {
+                ps.bmin[3 * i + y] = items[i].lo[y];
+                ps.bmax[3 * i + y] = items[i].hi[y];
+                ps.cen[3 * i + y] = items[i].c[y];
+            }
+        const RefBVH B = build_ref_bvh(ps, 2, 12);
+        // a slot: a BVH node (>= 0) or a pair (~index into items)
+        auto area = [&](int64_t r) {
+            const double* lo = r >= 0 ? &B.lo[3 * r] : items[~r].lo;
+            const double* hi = r >= 0 ? &B.hi[3 * r] : items[~r].hi;
+            const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+            return dx * dy + dy * dz + dz * dx;
+        };
+        auto expand = [&](int64_t r, std::vector<int64_t>& o) {
+            if (B.isLeaf(r)) {
+                for (int64_t q = 0; q < B.count[r]; ++q) o.push_back(~B.primIdx[B.leftFirst[r] + q]);
+            } else {
+                o.push_back(B.leftFirst[r]);
+                o.push_back(B.leftFirst[r] + 1);
+            }
+        };
+        auto size_of = [&](int64_t r) { return B.isLeaf(r) ? B.count[r] : 2; };
+        auto term = [&](int64_t r) { return r < 0 || (B.isLeaf(r) && B.count[r] == 1); };
+        std::function<void(int64_t, int64_t)> coll = [&](int64_t r, int64_t depth) {
+            out.depth = std::max(out.depth, depth);
+            std::vector<int64_t> c;
+            expand(r, c);
+            for (;;) {
+                int best = -1;
+                double bestA = -1.0;
+                for (size_t i = 0; i < c.size(); ++i) {
+                    if (term(c[i]) || c.size() - 1 + (size_t)size_of(c[i]) > 4) continue;
+                    const double ar = area(c[i]);
+                    if (ar > bestA) { bestA = ar; best = (int)i; }
+                }
+                if (best < 0) break;
+                std::vector<int64_t> e;
+                expand(c[best], e);
+                c.erase(c.begin() + best);
+                c.insert(c.begin() + best, e.begin(), e.end());
+            }
+            const size_t idx = out.nodes.size();
+            out.nodes.emplace_back();
+            int32_t refs[4] = {0, 0, 0, 0};
+            for (size_t i = 0; i < c.size(); ++i) {
+                if (term(c[i])) {
+                    const int64_t pi = c[i] < 0 ? ~c[i] : B.primIdx[B.leftFirst[c[i]]];
+                    refs[i] = ~(int32_t)out.pairs.size();
+                    out.pairs.push_back({items[pi].t0, items[pi].inst});
+                } else {
+                    refs[i] = (int32_t)out.nodes.size();
+                    coll(c[i], depth + 1);
+                }
+            }
+            W4Node& n = out.nodes[idx];
+            std::memset(&n, 0, sizeof(n));
+            for (int q = 0; q < 4; ++q) {
+                const bool has = q < (int)c.size();
+                const double* lo = !has ? nullptr : c[q] >= 0 ? &B.lo[3 * c[q]] : items[~c[q]].lo;
+                const double* hi = !has ? nullptr : c[q] >= 0 ? &B.hi[3 * c[q]] : items[~c[q]].hi;
+                for (int y = 0; y < 3; ++y) {
+                    n.pnear[y][q] = has ? WideBuilder::down(lo[y]) : HUGE_VALF;
+                    n.pfar[y][q] = has ? WideBuilder::up(hi[y]) : HUGE_VALF;
+                }
+                n.ref[q] = refs[q];
+            }
+        };
+        out.nodes.reserve(items.size() / 2 + 4);
+        coll(0, 1);
+    }
     if (3 * out.depth + 2 > kStackCap) return;
     const int64_t node_base = (int64_t)S.wnodes.size();
     for (W4Node n : out.nodes) {                         // node refs relative to the whole array
