@@ -117,6 +117,9 @@ __device__ __forceinline__ void walk_closest(const RenderParams& P, const V3& o,
 #ifndef MYRT_TW_PARK
 #define MYRT_TW_PARK 1
 #endif
+#ifndef MYRT_FIT_PARK
+#define MYRT_FIT_PARK 1      // the flattened-tree walks park the world ray too (read back at each pair)
+#endif
 template <bool COUNT, class Park>
 __device__ __forceinline__ void walk_closest_tw_parked(const RenderParams& P, const Park& pk, double tlo,
                                                        double time, Hit& h, Stack& st, Counts& c) {
@@ -162,7 +165,7 @@ __device__ __forceinline__ bool walk_occluded(const RenderParams& P, const V3& o
         const V3 inv = rcp(d);
         if (WIDE && __all(wide_ok(inv))) {
             bool tie = false;
-            if (PARK) {
+            if (PARK && MYRT_FIT_PARK) {
                 WPark pk;                                 // private memory, or the megakernel's LDS slots
                 pk.store(o, d);
                 return wide_walk<COUNT, true, true>(P, pk, inv, 0.0, tmax, hu, tie, st, c);
@@ -418,7 +421,8 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
         const V3 inv = rcp(d);
         Hit h;
         park();
-        if ((WALK == kWalkTransformed || WALK == kWalkFit) && MYRT_TW_PARK && (!BOUNCE || MYRT_BOUNCE_WIDE)) {
+        if ((WALK == kWalkTransformed || (WALK == kWalkFit && MYRT_FIT_PARK)) && MYRT_TW_PARK &&
+            (!BOUNCE || MYRT_BOUNCE_WIDE)) {
             TwPark pk;                                    // the world ray waits in private memory / LDS
             pk.store(o, d);
             if (WALK == kWalkFit) walk_closest_fit_parked<COUNT>(P, pk, tlo, time, h, st, c);
@@ -2186,7 +2190,18 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         const int64_t ql = s->opt[kOptQueueLevels];
         const int32_t levels = ql >= 0 ? (int32_t)std::min<int64_t>(ql, P.max_depth) : P.max_depth;
         for (int32_t level = 1; level <= levels; ++level) {
-#define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), qgrid, qblock, qlds, stream, P, level)
+            // the grid for the level's rays seen so far (the waves stride over however many there
+            // are): the sparse deep levels no longer dispatch a chip's worth of empty waves beside
+            // the other frames in flight
+#ifndef MYRT_QGRID_BY_HINT
+#define MYRT_QGRID_BY_HINT 1
+#endif
+            dim3 lgrid = qgrid;
+            if (MYRT_QGRID_BY_HINT && r.qhint[level] > 0) {
+                const int64_t batches = (kQRegions * r.qhint[level] + r.qhint[level] / 4 + 63) / 64;
+                lgrid.x = (unsigned)std::max<int64_t>(r.cus, std::min<int64_t>((int64_t)qgrid.x, batches));
+            }
+#define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), lgrid, qblock, qlds, stream, P, level)
             MYRT_BY_WALK(MYRT_QB);
 #undef MYRT_QB
         }
