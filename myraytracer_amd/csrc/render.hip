@@ -388,7 +388,7 @@ typedef TwParked TwPark;
 // `park_rng`: the PCG32 state waits in this lane's LDS pixel slot 3 while the rays are traced
 // (BOUNCE) instead of being live - spilled - across the walks
 // QUEUE (primary pass of the compacted bounce render, !BOUNCE): a mirror/conductor hit writes
-// its reflected ray to a level-1 record (q_reserve, region `qregion`) and sets `deferred`;
+// its reflected ray to a level-1 record (q_reserve, region = its block's) and sets `deferred`;
 // k_bounce delivers that pixel.  The record index waits in pixel slot 0 (the sample sum, written
 // only after trace_path) across the shadow walks.  The PCG32 state is read from pixel slot 3
 // (the caller parks it there) and (i0, j0) + the lane give its stream.
@@ -401,7 +401,7 @@ typedef TwParked TwPark;
 template <bool COUNT, bool BOUNCE, int WALK, bool QUEUE = false>
 __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double time, PCG32& rng, Stack& st,
                          Counts& c, bool park_rng, int i0 = 0, int j0 = 0,
-                         bool* deferred = nullptr, int qregion = 0) {
+                         bool* deferred = nullptr) {
     static_assert(!(QUEUE && BOUNCE), "the queued primary pass has no bounce loop");
     // flattened-tree scenes are static (scene.cpp build_wide_tw): motion * time == 0 for every time in
     // [0, 1), so the ray time need not stay live (the caller still draws it: the PCG32 sequence)
@@ -450,23 +450,24 @@ __device__ V3 trace_path(const RenderParams& P, V3 o, V3 d, double tlo, double t
             const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && P.max_depth > 0;
             const unsigned long long m = __ballot(want);
             if (m) {
-                // the wave's records with one atomic, formed while it returns (the secondary-ray
-                // count is k_queue_done's)
-                const QTicket tk = q_issue(P, 1, qregion, m);
-                QRay qr{};
-                int i = 0, j = 0;
-                if (want) {
-                    const int l = pix_lane();                     // the lane's pixel, recomputed
-                    i = i0 + l % kTileW; j = j0 + l / kTileW;
-                    PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*pix_slot(3)),
-                                            pixel_seed(i, j));
-                    qr = queue_ray(P, M, d, N, p, r);
-                }
-                const long long q = q_index(P, 1, qregion, m, want, tk);
+                // the wave's records with one atomic in its region (the block's, recomputed: a
+                // region kept live from the caller, or the ray formed while the atomic returns,
+                // spilled - 417 vs 180 MB of writes per C5 frame); the secondary-ray count is
+                // k_queue_done's
+                const int region = (int)(blockIdx.x % kQRegions);
+                const QTicket tk = q_issue(P, 1, region, m);
+                const long long q = q_index(P, 1, region, m, want, tk);
                 if (want) {
                     queued = true;
                     *pix_slot(0) = __builtin_bit_cast(double, q);  // not live across the shadow walks
-                    if (q >= 0) queue_store(P, q, qr, time, i, j, -1);
+                    if (q >= 0) {
+                        const int l = pix_lane();                 // the lane's pixel, recomputed
+                        const int i = i0 + l % kTileW, j = j0 + l / kTileW;
+                        PCG32 r = PCG32::resume(__builtin_bit_cast(unsigned long long, (double)*pix_slot(3)),
+                                                pixel_seed(i, j));
+                        const QRay qr = queue_ray(P, M, d, N, p, r);
+                        queue_store(P, q, qr, time, i, j, -1);
+                    }
                 }
             }
         }
@@ -652,7 +653,7 @@ __global__ __launch_bounds__(256) MYRT_MEGA_ATTR void render_kernel(RenderParams
             // across the walks; the memory clobber makes the reloads real loads.
             if (!BOUNCE) *pix_slot(3) = __builtin_bit_cast(double, rng.state);
             const V3 col = trace_path<COUNT, BOUNCE, WALK, QUEUE>(P, camEye, dir, tlo, time, rng, st, cnt, true,
-                                                                 i0, j0, &deferred, (int)(blockIdx.x % kQRegions));
+                                                                 i0, j0, &deferred);
             asm volatile("" ::: "memory");
             if (!BOUNCE) {
                 const int l2 = pix_lane();
@@ -2190,18 +2191,8 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         const int64_t ql = s->opt[kOptQueueLevels];
         const int32_t levels = ql >= 0 ? (int32_t)std::min<int64_t>(ql, P.max_depth) : P.max_depth;
         for (int32_t level = 1; level <= levels; ++level) {
-            // the grid for the level's rays seen so far (the waves stride over however many there
-            // are): the sparse deep levels no longer dispatch a chip's worth of empty waves beside
-            // the other frames in flight
-#ifndef MYRT_QGRID_BY_HINT
-#define MYRT_QGRID_BY_HINT 1
-#endif
-            dim3 lgrid = qgrid;
-            if (MYRT_QGRID_BY_HINT && r.qhint[level] > 0) {
-                const int64_t batches = (kQRegions * r.qhint[level] + r.qhint[level] / 4 + 63) / 64;
-                lgrid.x = (unsigned)std::max<int64_t>(r.cus, std::min<int64_t>((int64_t)qgrid.x, batches));
-            }
-#define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), lgrid, qblock, qlds, stream, P, level)
+            // (a grid sized by the level's ray-count hint measured neutral: profiles/r06q_ab_c5.txt)
+#define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), qgrid, qblock, qlds, stream, P, level)
             MYRT_BY_WALK(MYRT_QB);
 #undef MYRT_QB
         }

@@ -414,6 +414,18 @@ __device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int
 #else
 #define MYRT_FULL_ATTR
 #endif
+// render_full alone (the combine pass over the logged hits, with its per-lane trace() frames): 2
+// waves/SIMD - its 256 VGPRs hold what 4 waves spilled (112 spills, ~1 GB of writes per C3g
+// frame): C3g 3.20 -> 3.12, C3r 3.80 -> 3.72 ms per frame (3 waves: 3.16 / 3.80;
+// profiles/r06s_ab_c3g.txt, r06s_ab_c3r.txt)
+#ifndef MYRT_RF_WPE
+#define MYRT_RF_WPE 2
+#endif
+#if MYRT_RF_WPE > 0
+#define MYRT_RF_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_RF_WPE)))
+#else
+#define MYRT_RF_ATTR
+#endif
 // The closest-hit walks' equal-t re-walks (wide.h ties; rt_stats.rewalked) of one wave, counted
 // where the walks run (every lane of the wave must reach this: wave_sum reads all 64 lanes).
 __device__ __forceinline__ void flush_ties(const RenderParams& P, const Counts& c) {
@@ -720,7 +732,7 @@ __global__ __launch_bounds__(256) void k_jscan(RenderParams P) {
 
 // Pass 3 (or the only pass without area lights): the render.
 template <bool COUNT, bool DEEP, int WALK>
-__global__ __launch_bounds__(256) MYRT_FULL_ATTR void render_full(RenderParams P) {
+__global__ __launch_bounds__(256) MYRT_RF_ATTR void render_full(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
