@@ -414,6 +414,15 @@ __device__ __forceinline__ void full_pixel_of(const RenderParams& P, int& i, int
 #else
 #define MYRT_FULL_ATTR
 #endif
+// k_events alone (the depth-first events pass of rough / deep frames)
+#ifndef MYRT_EV_WPE
+#define MYRT_EV_WPE MYRT_FULL_WPE
+#endif
+#if MYRT_EV_WPE > 0
+#define MYRT_EV_ATTR __attribute__((amdgpu_waves_per_eu(MYRT_EV_WPE)))
+#else
+#define MYRT_EV_ATTR
+#endif
 // render_full alone (the combine pass over the logged hits, with its per-lane trace() frames): 2
 // waves/SIMD - its 256 VGPRs hold what 4 waves spilled (112 spills, ~1 GB of writes per C3g
 // frame): C3g 3.20 -> 3.12, C3r 3.80 -> 3.72 ms per frame (3 waves: 3.16 / 3.80;
@@ -434,7 +443,7 @@ __device__ __forceinline__ void flush_ties(const RenderParams& P, const Counts& 
 }
 
 template <bool DEEP, int WALK>
-__global__ __launch_bounds__(256) MYRT_FULL_ATTR void k_events(RenderParams P) {
+__global__ __launch_bounds__(256) MYRT_EV_ATTR void k_events(RenderParams P) {
     extern __shared__ unsigned long long lds_stack[];
     int i, j, slot, row;
     full_pixel_of(P, i, j, slot, row);
