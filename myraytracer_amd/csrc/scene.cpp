@@ -703,8 +703,8 @@ static void build_wide(HostScene& S) {
 }
 
 // Flattened instance tree (transformed scenes; wide.h fit_walk).  One four-wide tree in WORLD
-// space over every (instance, BLAS leaf run) pair, built by binned SAH over the pairs' world boxes
-// (split in two, each half in two again: up to four slots a node), so that the terrain's leaves
+// space over every (instance, BLAS leaf run) pair - the reference's binned SAH builder over the
+// pairs' world boxes, collapsed to four-wide nodes like C3's tree - so that the terrain's leaves
 // and the sphere instances' leaves interleave in one walk as an identity scene's do.  A pair's
 // box is AABB.transformed (AABB.swift:71-92) of its local leaf box: the eight corners through
 // localToWorld, min/max.  The walk tests the reference's boxes exactly (FP64) before it accepts a
@@ -786,151 +786,20 @@ static void build_fit(HostScene& S) {
         }
     }
     if (items.empty() || !std::isfinite(coord) || items.size() >= (size_t(1) << 30)) return;
-    // binned SAH split of items [a, b) into [a, m), [m, b) (object median when no bin split helps);
-    // one pass bins all three axes
-    constexpr int kBins = 16;
-    auto split = [&](size_t a, size_t b) -> size_t {
-        double cl[3] = {kInf, kInf, kInf}, ch[3] = {-kInf, -kInf, -kInf};
-        for (size_t i = a; i < b; ++i)
-            for (int x = 0; x < 3; ++x) { cl[x] = fmn(cl[x], items[i].c[x]); ch[x] = fmx(ch[x], items[i].c[x]); }
-        double sc[3];
-        for (int x = 0; x < 3; ++x) sc[x] = ch[x] > cl[x] ? kBins / (ch[x] - cl[x]) : 0.0;
-        int cnt[3][kBins] = {};
-        double blo[3][kBins][3], bhi[3][kBins][3];
-        for (int x = 0; x < 3; ++x)
-            for (int q = 0; q < kBins; ++q)
-                for (int y = 0; y < 3; ++y) { blo[x][q][y] = kInf; bhi[x][q][y] = -kInf; }
-        for (size_t i = a; i < b; ++i) {
-            const Item& it = items[i];
-            for (int x = 0; x < 3; ++x) {
-                const int q = std::min(kBins - 1, (int)((it.c[x] - cl[x]) * sc[x]));
-                cnt[x][q]++;
-                for (int y = 0; y < 3; ++y) {
-                    blo[x][q][y] = fmn(blo[x][q][y], it.lo[y]);
-                    bhi[x][q][y] = fmx(bhi[x][q][y], it.hi[y]);
-                }
-            }
-        }
-        double best = kInf;
-        int bax = -1, bb = 0;
-        for (int x = 0; x < 3; ++x) {
-            if (!(ch[x] > cl[x])) continue;
-            double ra[kBins];
-            {
-                double lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
-                int n = 0;
-                for (int q = kBins - 1; q >= 1; --q) {
-                    n += cnt[x][q];
-                    for (int y = 0; y < 3; ++y) { lo[y] = fmn(lo[y], blo[x][q][y]); hi[y] = fmx(hi[y], bhi[x][q][y]); }
-                    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-                    ra[q] = n ? n * (dx * dy + dy * dz + dz * dx) : 0.0;
-                }
-            }
-            double lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
-            int n = 0;
-            for (int q = 0; q < kBins - 1; ++q) {
-                n += cnt[x][q];
-                for (int y = 0; y < 3; ++y) { lo[y] = fmn(lo[y], blo[x][q][y]); hi[y] = fmx(hi[y], bhi[x][q][y]); }
-                if (n == 0 || n == (int)(b - a)) continue;
-                const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-                const double cost = n * (dx * dy + dy * dz + dz * dx) + ra[q + 1];
-                if (cost < best) { best = cost; bax = x; bb = q; }
-            }
-        }
-        if (bax < 0) return a + (b - a) / 2;
-        const double s0 = sc[bax], c0 = cl[bax];
-        auto mid = std::partition(items.begin() + (ptrdiff_t)a, items.begin() + (ptrdiff_t)b, [&](const Item& it) {
-            return std::min(kBins - 1, (int)((it.c[bax] - c0) * s0)) <= bb;
-        });
-        const size_t m = (size_t)(mid - items.begin());
-        return (m == a || m == b) ? a + (b - a) / 2 : m;
-    };
-    // A subtree: its nodes in preorder (node refs local to `nodes`, terminal slots ~index into `pairs`).
-    // The top two levels build their subtrees on threads of their own, into their own FitOut, and
-    // the parent appends them in slot order: the result does not depend on scheduling.
+    // A subtree: its nodes in preorder (node refs local to `nodes`, terminal slots ~index into `pairs`)
     struct FitOut {
         std::vector<W4Node> nodes;
         std::vector<DFitPair> pairs;
         int64_t depth = 0;
     };
-    std::function<void(size_t, size_t, int64_t, FitOut&, int)> node = [&](size_t a, size_t b, int64_t depth, FitOut& out,
-                                                                         int par) {
-        out.depth = std::max(out.depth, depth);
-        size_t cut[5] = {a, a, b, b, b};
-        int nc;
-        if (b - a <= 4) {
-            nc = (int)(b - a);
-            for (int c = 0; c <= nc; ++c) cut[c] = a + (size_t)c;
-        } else {
-            const size_t m = split(a, b);
-            const size_t m0 = (m - a >= 2) ? split(a, m) : m;
-            const size_t m1 = (b - m >= 2) ? split(m, b) : b;
-            nc = 0;
-            cut[nc++] = a;
-            if (m0 != m) cut[nc++] = m0;
-            cut[nc++] = m;
-            if (m1 != b) cut[nc++] = m1;
-            cut[nc] = b;
-        }
-        const size_t idx = out.nodes.size();
-        out.nodes.emplace_back();
-        int32_t refs[4] = {0, 0, 0, 0};
-        double blo[4][3], bhi[4][3];
-        FitOut sub[4];
-        std::vector<std::thread> th;
-        for (int c = 0; c < nc; ++c) {
-            for (int y = 0; y < 3; ++y) { blo[c][y] = kInf; bhi[c][y] = -kInf; }
-            for (size_t i = cut[c]; i < cut[c + 1]; ++i)
-                for (int y = 0; y < 3; ++y) { blo[c][y] = fmn(blo[c][y], items[i].lo[y]); bhi[c][y] = fmx(bhi[c][y], items[i].hi[y]); }
-            if (cut[c + 1] - cut[c] == 1) {
-                refs[c] = ~(int32_t)out.pairs.size();
-                out.pairs.push_back({items[cut[c]].t0, items[cut[c]].inst});
-            } else if (par > 0 && cut[c + 1] - cut[c] >= 4096) {
-                th.emplace_back([&, c] { node(cut[c], cut[c + 1], depth + 1, sub[c], par - 1); });
-            } else if (par > 0) {
-                node(cut[c], cut[c + 1], depth + 1, sub[c], 0);
-            } else {                                     // serial: the subtree follows in place
-                refs[c] = (int32_t)out.nodes.size();
-                node(cut[c], cut[c + 1], depth + 1, out, 0);
-            }
-        }
-        for (auto& t : th) t.join();
-        for (int c = 0; c < nc; ++c) {                   // append the subtrees in slot order
-            if (sub[c].nodes.empty()) continue;
-            const int32_t nb = (int32_t)out.nodes.size(), pb = (int32_t)out.pairs.size();
-            for (W4Node n : sub[c].nodes) {
-                for (int q = 0; q < 4; ++q) {
-                    if (!(n.pnear[0][q] < HUGE_VALF)) continue;   // empty slot
-                    n.ref[q] = n.ref[q] >= 0 ? n.ref[q] + nb : ~(~n.ref[q] + pb);
-                }
-                out.nodes.push_back(n);
-            }
-            out.pairs.insert(out.pairs.end(), sub[c].pairs.begin(), sub[c].pairs.end());
-            out.depth = std::max(out.depth, sub[c].depth);
-            refs[c] = nb;
-            FitOut().nodes.swap(sub[c].nodes);
-        }
-        W4Node& n = out.nodes[idx];
-        std::memset(&n, 0, sizeof(n));
-        for (int q = 0; q < 4; ++q) {
-            for (int y = 0; y < 3; ++y) {
-                n.pnear[y][q] = q < nc ? WideBuilder::down(blo[q][y]) : HUGE_VALF;
-                n.pfar[y][q] = q < nc ? WideBuilder::up(bhi[q][y]) : HUGE_VALF;
-            }
-            n.ref[q] = refs[q];
-        }
-    };
     if (items.size() < 2) return;                        // one pair alone: tw_walk
     FitOut out;
-#ifndef MYRT_FIT_BUILD
-#define MYRT_FIT_BUILD 1
-#endif
-    if (MYRT_FIT_BUILD == 0) {
-        node(0, items.size(), 1, out, 2);
-    } else {
+    {
         // The reference's binned SAH builder (build_ref_bvh, BVH.swift:128-250) over the pairs'
         // world boxes, collapsed to four-wide nodes as build_wide collapses C3's tree: a node opens
         // its largest child while the children fit four slots; every pair is one terminal slot.
+        // (A direct four-way binned SAH - split in two, each half in two - ran C3i 1 % slower:
+        // profiles/r06o_ab_c3i_fit_builder.txt.)
         PrimSet ps;
         ps.n = (int64_t)items.size();
         ps.bmin.resize(3 * items.size()); ps.bmax.resize(3 * items.size()); ps.cen.resize(3 * items.size());

@@ -291,17 +291,10 @@ __device__ __forceinline__ void fit_local(const RenderParams& P, int k, const V3
 // per-iteration divergence (inner step / leaf run), as the binary walk's counters.
 // FIT: the flattened instance tree of a transformed scene (above): terminal slots are pairs.
 //
-// Postponed leaf runs (MYRT_POSTPONE = T > 0; Aila-Laine speculative traversal): a lane that
-// reaches a leaf run parks it and keeps stepping inner nodes (with its current, larger pruning
-// limit); the wave runs the parked leaf runs together once at least T lanes hold one, or when
-// no lane can take an inner step (its stack is empty, or it holds a parked run and has met a
-// second).  Only the order in which leaf runs are tested changes, and with it only which of
-// several EQUAL-t candidates is met first - those lanes raise `tie` whatever the order and are
-// re-walked in the reference's order - while the pruning limit stays >= the current hit's t at
-// every test, so no leaf whose box holds the final hit is pruned: the header's argument holds.
-#ifndef MYRT_POSTPONE
-#define MYRT_POSTPONE 0
-#endif
+// (Postponed leaf runs - Aila-Laine speculative traversal: a lane parks its leaf run and keeps
+// stepping inner nodes until enough lanes hold one - measured 8,368 -> 6,631..6,941 Mrays/s on C3
+// at thresholds of 16..64 lanes, profiles/r06a_ab_c3_postpone.txt: a closest-hit walk that defers
+// its leaves keeps its pruning limit high.  Removed; git history keeps it.)
 // W: the ray, kept by the caller (TwWorld) or parked (fit walks of the megakernels: the world ray
 // is read back at a pair, where its local ray is formed, and not live across the walk).
 template <bool COUNT, bool SHADOW, bool FIT = false, class World = TwWorld>
@@ -377,40 +370,6 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const World& W,
         };
         return ctris ? run(ctris) : run(tris);
     };
-#if MYRT_POSTPONE
-    bool live = true;                                      // ref holds a node or a leaf run to visit
-    int pend = 0;                                          // the parked leaf run (a negative ref)
-    bool hasp = false;
-    for (;;) {
-        const bool step = live && ref >= 0;
-        if (COUNT) {
-            const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
-            c.it_wave_inner[SHADOW] += (first && __ballot(step)) ? 1 : 0;
-            c.it_lane_inner[SHADOW] += step ? 1 : 0;
-            if (SHADOW) c.it_shadow++; else c.it_closest++;
-            if (step) c.recs++;
-        }
-        if (step) {
-            if (!wide_inner(P, wbase, ref, R, lim, st)) live = wide_pop(st, base, lim, ref);
-        } else if (live && !hasp) {
-            pend = ref;
-            hasp = true;
-            live = wide_pop(st, base, lim, ref);
-        }
-        if (__popcll(__ballot(hasp)) >= MYRT_POSTPONE || !__any(live && (ref >= 0 || !hasp))) {
-            if (COUNT) {
-                const bool first = (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1));
-                c.it_wave_leaf[SHADOW] += (first && __ballot(hasp)) ? 1 : 0;
-                c.it_lane_leaf[SHADOW] += hasp ? 1 : 0;
-            }
-            if (hasp) {
-                hasp = false;
-                if (leaf(~pend)) { occ = true; live = false; }
-            }
-        }
-        if (!__any(live || hasp)) break;
-    }
-#else
     for (;;) {
         if (COUNT) {
             const bool in = ref >= 0;
@@ -431,7 +390,6 @@ __device__ __forceinline__ bool wide_walk(const RenderParams& P, const World& W,
         }
         if (!wide_pop(st, base, lim, ref)) break;
     }
-#endif
     st.reset(base);
     return occ;
 }
