@@ -17,12 +17,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 sc = (scenes.scene_c3 if cfg == "c3" else scenes.scene_c5)(path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
+for kv in filter(None, os.environ.get("PROBE_OPT", "").split(",")):   # e.g. PROBE_OPT=tile_order=100
+    k, v = kv.split("=")
+    eng.set_option(k, int(v))
 W, H = sc.cameras[0].image_resolution
 QS = [int(x) for x in os.environ.get("PROBE_Q", "1,4,8").split(",")]
 NS = [int(x) for x in os.environ.get("PROBE_N", "2,4,8").split(",")]
 Q = max(QS + [4])
 fbs = [M.pinned_array((H, W, 4), np.uint8) for _ in range(Q)]
-K = 40
+K = int(os.environ.get("PROBE_K", "40"))
 
 
 def t_pipe(first, step, q):
