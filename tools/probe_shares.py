@@ -17,6 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CFG = os.environ.get("PROBE_CFG", "c3")
 sc = (scenes.scene_c3 if CFG == "c3" else scenes.scene_c5)(path_dir=os.path.join(ROOT, "scenes_cache"))
 eng = M.RayTracerEngine(sc)
+for kv in filter(None, os.environ.get("PROBE_OPT", "").split(",")):   # e.g. PROBE_OPT=submit_counters=0
+    k, v = kv.split("=")
+    eng.set_option(k, int(v))
 W, H = sc.cameras[0].image_resolution
 N = int(os.environ.get("PROBE_N", "8"))
 Q = int(os.environ.get("PROBE_Q", "16"))
