@@ -213,6 +213,8 @@ int32_t rt_scene_info_get(const rt_scene* scene, rt_scene_info* out);
  *   tile_order (0)       % of tile groups dispatched slowest first
  *   fit (1)              transformed scenes: the flattened instance tree (wide.h fit_walk);
  *                        0 = the TLAS / per-BLAS four-wide walk (tw_walk)
+ *   queue_tail (2)       compacted bounce render: levels >= this one traced depth-first in one
+ *                        launch (render.hip k_bounce_tail); 0 = one launch per level
  * Unknown names and out-of-range values return RT_ERR_INVALID_ARG.  Set options between
  * renders (not while renders of the scene are in flight).  The test hooks below are refused
  * here (RT_ERR_INVALID_ARG); rt_scene_get_option reads every option. */

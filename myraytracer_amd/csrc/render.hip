@@ -754,6 +754,21 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long x
     return t;
 }
 
+// A sample whose ray of record g (level `level`) ended with radiance L: back along the parents,
+// Lo_k + M_k * L_(k+1) with the NaN guard per level, and the pixel stored.
+__device__ __forceinline__ void q_resolve(const RenderParams& P, long long g, int level, V3 L) {
+    int pi = 0, pj = 0;
+    for (int lev = level; lev >= 1; --lev) {
+        const BounceRec& Q = P.bounce[g];
+        const V3 Lq = ld3(Q.Lo) + ld3(Q.M) * L;
+        L = isfin(Lq) ? Lq : v3(0, 0, 0);
+        pi = Q.i; pj = Q.j;
+        g = Q.parent;
+    }
+    const V3 pixel = v3(0.0 + L.x, 0.0 + L.y, 0.0 + L.z);   // the sample sum (one sample)
+    store_pixel(P, pi, pj, pixel / (double)P.cam.samples);
+}
+
 // One level of the compacted bounce render: the rays trace(depth = level), one lane per ray;
 // wave w of the grid takes the batches of 64 consecutive records w, w + G, ... of the level's
 // regions laid end to end (lane r < kQRegions holds region r's count, clamped to the capacity,
@@ -765,36 +780,52 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long x
 #ifndef MYRT_QUEUE_WPE
 #define MYRT_QUEUE_WPE 4
 #endif
-template <int WALK>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_WPE))) void k_bounce(RenderParams P,
-                                                                                                    int level) {
-    extern __shared__ unsigned long long lds_stack[];
+// A level's records as one list: lane r < kQRegions holds region r's count (k_bounce(level - 1) /
+// the primary pass), clamped to the capacity, and its exclusive prefix `ex`; T = the level's rays.
+struct QLevel { unsigned long long cap, lbase; unsigned ex, T; };
+__device__ __forceinline__ QLevel q_level(const RenderParams& P, int level) {
     const int lane = threadIdx.x & 63;
-    Counts cnt{};
-    const unsigned long long cap = P.qhdr[kQHdrCap + level], lbase = P.qhdr[level];
-    const unsigned long long cr = lane < kQRegions ? *q_counter(P, level, lane) : 0ull;   // k_bounce(level - 1) / primary pass
-    const unsigned c = (unsigned)(cr < cap ? cr : cap);
+    QLevel Q;
+    Q.cap = P.qhdr[kQHdrCap + level];
+    Q.lbase = P.qhdr[level];
+    const unsigned long long cr = lane < kQRegions ? *q_counter(P, level, lane) : 0ull;
+    const unsigned c = (unsigned)(cr < Q.cap ? cr : Q.cap);
     unsigned inc = c;                                    // inclusive prefix over the regions
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const unsigned y = (unsigned)__shfl_up((int)inc, off, 64);
         if (lane >= off) inc += y;
     }
-    const unsigned ex = inc - c;
-    const unsigned T = (unsigned)__shfl((int)inc, 63, 64);
+    Q.ex = inc - c;
+    Q.T = (unsigned)__shfl((int)inc, 63, 64);
+    return Q;
+}
+// ray b of the list (every lane of the wave calls it): its record and region jl, the last region
+// with ex <= b
+__device__ __forceinline__ long long q_record(const QLevel& Q, unsigned b, int& jl) {
+    jl = 0;
+    int jh = kQRegions;
+#pragma unroll
+    for (int s = 0; s < kQRegionBits; ++s) {
+        const int mid = (jl + jh) >> 1;
+        if ((unsigned)__shfl((int)Q.ex, mid, 64) <= b) jl = mid; else jh = mid;
+    }
+    return (long long)(Q.lbase + (unsigned long long)jl * Q.cap + (unsigned long long)(b - (unsigned)__shfl((int)Q.ex, jl, 64)));
+}
+template <int WALK>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_WPE))) void k_bounce(RenderParams P,
+                                                                                                    int level) {
+    extern __shared__ unsigned long long lds_stack[];
+    const int lane = threadIdx.x & 63;
+    Counts cnt{};
+    const QLevel ql = q_level(P, level);
     MYRT_STACK(st, lds_stack);
     st.uni_spill = true;
-    for (unsigned x0 = blockIdx.x * 64u; x0 < T; x0 += gridDim.x * 64u) {
+    for (unsigned x0 = blockIdx.x * 64u; x0 < ql.T; x0 += gridDim.x * 64u) {
         const unsigned b = x0 + (unsigned)lane;          // this lane's ray
-        int jl = 0, jh = kQRegions;                      // its region: the last one with ex <= b
-#pragma unroll
-        for (int s = 0; s < kQRegionBits; ++s) {
-            const int mid = (jl + jh) >> 1;
-            if ((unsigned)__shfl((int)ex, mid, 64) <= b) jl = mid; else jh = mid;
-        }
-        const long long g = (long long)(lbase + (unsigned long long)jl * cap +
-                                        (unsigned long long)(b - (unsigned)__shfl((int)ex, jl, 64)));
-        if (b >= T) continue;
+        int jl;
+        const long long g = q_record(ql, b, jl);
+        if (b >= ql.T) continue;
         const BounceRec& R = P.bounce[g];
         const V3 o = ld3(R.o), d = ld3(R.d);
         const double time = (WALK == kWalkIdentity || WALK == kWalkFit) ? 0.0 : R.time;
@@ -851,23 +882,84 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_W
             if (!want) L = isfin(Lo) ? Lo : v3(0, 0, 0);
             else if (q >= 0) queue_write_lo(P, q, Lo);
         }
-        if (!want) {     // back along the parents: Lo_k + M_k * L_(k+1), NaN guard per level
-            int pi = 0, pj = 0;
-            long long gg = g;
-            for (int lev = level; lev >= 1; --lev) {
-                const BounceRec& Q = P.bounce[gg];
-                const V3 Lq = ld3(Q.Lo) + ld3(Q.M) * L;
-                L = isfin(Lq) ? Lq : v3(0, 0, 0);
-                pi = Q.i; pj = Q.j;
-                gg = Q.parent;
-            }
-            const V3 pixel = v3(0.0 + L.x, 0.0 + L.y, 0.0 + L.z);   // the sample sum (one sample)
-            store_pixel(P, pi, pj, pixel / (double)P.cam.samples);
-        }
+        if (!want) q_resolve(P, g, level, L);
     }
     const unsigned long long s0 = wave_sum(cnt.shadow), s2 = wave_sum(cnt.shadow_traced), s3 = wave_sum(cnt.ties);
     if (lane == 0) {
         if (s0) atomicAdd(&P.counters[0], s0);
+        if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
+        if (s3) atomicAdd(&P.counters[kCounterTies], s3);
+    }
+}
+
+// The sparse last levels of the compacted bounce render in one launch (option queue_tail): each
+// lane takes one ray of `level` and traces its whole subtree depth-first - the reflected ray of a
+// mirror/conductor hit below maxRecursionDepth is traced by the same lane, its Lo and multiplier
+// kept per level - instead of a level launch each (at C5's levels 2-4 a launch is ~0.2 ms of one
+// ray's latency for a few thousand rays).  The values and operations are k_bounce's: the PCG32
+// stream continues from the record, the sample is combined backward with the per-level NaN
+// guard, then along the parent records (q_resolve).  Its bounces count as secondary rays here
+// (k_queue_done counts the reserved records).
+template <int WALK>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MYRT_QUEUE_WPE))) void k_bounce_tail(
+    RenderParams P, int level) {
+    extern __shared__ unsigned long long lds_stack[];
+    const int lane = threadIdx.x & 63;
+    Counts cnt{};
+    const QLevel ql = q_level(P, level);
+    MYRT_STACK(st, lds_stack);
+    st.uni_spill = true;
+    for (unsigned x0 = blockIdx.x * 64u; x0 < ql.T; x0 += gridDim.x * 64u) {
+        const unsigned b = x0 + (unsigned)lane;
+        int jl;
+        const long long g = q_record(ql, b, jl);
+        if (b >= ql.T) continue;
+        const BounceRec& R = P.bounce[g];
+        V3 o = ld3(R.o), d = ld3(R.d);
+        const double time = (WALK == kWalkIdentity || WALK == kWalkFit) ? 0.0 : R.time;
+        PCG32 rng = PCG32::resume(R.rng, pixel_seed(R.i, R.j));
+        V3 Lst[kMaxQueueLevels], Mst[kMaxQueueLevels];
+        int k = 0;                                       // levels below `level` traced by this lane
+        V3 L = v3(0, 0, 0);
+        for (;;) {
+            if (!P.has_tlas) break;
+            const V3 inv = rcp(d);
+            Hit h;
+            walk_closest<false, WALK>(P, o, d, inv, 0.0, time, h, st, cnt);
+            if (h.inst < 0) { L = ld3(P.background); break; }
+            V3 p, Ngeo;
+            hit_geometry<false>(P, o, d, time, h, p, Ngeo, cnt);
+            const DInstance& I = P.insts[h.inst];
+            const DMaterial& M = P.mats[max(0, min(P.num_mats - 1, I.material - 1))];
+            const bool frontFacing = dot(d, Ngeo) < 0;
+            const V3 N = frontFacing ? Ngeo : -Ngeo;
+            const bool computeDirect = !(M.ior > 0) || frontFacing;
+            V3 Lo = computeDirect ? ld3(P.ambient) * ld3(M.ambient) : v3(0, 0, 0);
+            const bool want = (M.type == RT_MAT_MIRROR || M.type == RT_MAT_CONDUCTOR) && level + k < P.max_depth &&
+                              k < kMaxQueueLevels;
+            QRay qr{};
+            if (want) qr = queue_ray(P, M, d, N, p, rng);
+            auto none = []() {};
+            if (computeDirect) point_lights<false, WALK, true>(P, M, N, p, d, time, st, cnt, Lo, none, none);
+            if (!want) { L = isfin(Lo) ? Lo : v3(0, 0, 0); break; }
+            Lst[k] = Lo;
+            Mst[k] = qr.mult;
+            ++k;
+            cnt.secondary++;
+            o = qr.o;
+            d = qr.d;
+        }
+        for (int q = k - 1; q >= 0; --q) {
+            const V3 Lq = Lst[q] + Mst[q] * L;
+            L = isfin(Lq) ? Lq : v3(0, 0, 0);
+        }
+        q_resolve(P, g, level, L);
+    }
+    const unsigned long long s0 = wave_sum(cnt.shadow), s1 = wave_sum(cnt.secondary),
+                             s2 = wave_sum(cnt.shadow_traced), s3 = wave_sum(cnt.ties);
+    if (lane == 0) {
+        if (s0) atomicAdd(&P.counters[0], s0);
+        if (s1) atomicAdd(&P.counters[1], s1);
         if (s2) atomicAdd(&P.counters[kCounterShadowTraced], s2);
         if (s3) atomicAdd(&P.counters[kCounterTies], s3);
     }
@@ -1261,7 +1353,7 @@ enum OptId {
     kOptWide, kOptUnified, kOptUnifiedTransformed, kOptCompactRecords, kOptCompactTris, kOptXcdGroup,
     kOptQueue, kOptQueueLevels, kOptHitlog, kOptNodeshade, kOptLevels, kOptTreePpw, kOptFullFlights,
     kOptDeepCapMb, kOptBatches, kOptZerocopy, kOptSubmitEvents, kOptSubmitCounters, kOptSubmitDma,
-    kOptDebugFailReplica, kOptWideDeltaScale, kOptNodeLists, kOptTileOrder, kOptFit, kOptCount
+    kOptDebugFailReplica, kOptWideDeltaScale, kOptNodeLists, kOptTileOrder, kOptFit, kOptQueueTail, kOptCount
 };
 // `unsafe` options are test hooks: rt_scene_set_option refuses them (RT_ERR_INVALID_ARG); only the
 // non-production entry point rt_scene_set_unsafe_option sets them (rtcore.h).
@@ -1293,6 +1385,8 @@ static const OptDef kOptDefs[kOptCount] = {
     {"node_lists", 1, 0, 1},              // level passes past 0 and node shading over compacted node lists
     {"tile_order", 0, 0, 100},            // % of XCD tile groups dispatched first, slowest first (TileOrder; 0 = row-major)
     {"fit", 1, 0, 1},                     // transformed scenes: the flattened instance tree (wide.h fit_walk; 0 = tw_walk)
+    {"queue_tail", 2, 0, 15},             // compacted bounce render: levels >= this one in one k_bounce_tail launch (0 = a launch per level;
+                                          // C5 one frame 3.49 -> 3.23 ms, pipelined +0.2 %: profiles/r06t_ab_c5_tail.txt, r06u_ab_c5_tail.txt)
 };
 
 struct rt_scene {
@@ -2190,10 +2284,17 @@ static int32_t launch(const rt_scene* s, DeviceReplica& r, const RenderParams& P
         // option queue_levels (timing probe only: frames are incomplete below max_depth)
         const int64_t ql = s->opt[kOptQueueLevels];
         const int32_t levels = ql >= 0 ? (int32_t)std::min<int64_t>(ql, P.max_depth) : P.max_depth;
+        const int64_t tail = s->opt[kOptQueueTail];
         for (int32_t level = 1; level <= levels; ++level) {
             // (a grid sized by the level's ray-count hint measured neutral: profiles/r06q_ab_c5.txt)
 #define MYRT_QB(W_) hipLaunchKernelGGL((dev::k_bounce<W_>), qgrid, qblock, qlds, stream, P, level)
+#define MYRT_QT(W_) hipLaunchKernelGGL((dev::k_bounce_tail<W_>), qgrid, qblock, qlds, stream, P, level)
+            if (tail > 0 && level >= tail) {
+                MYRT_BY_WALK(MYRT_QT);
+                break;
+            }
             MYRT_BY_WALK(MYRT_QB);
+#undef MYRT_QT
 #undef MYRT_QB
         }
         hipLaunchKernelGGL(dev::k_queue_done, dim3(1), dim3(64), 0, stream, P, (int)P.max_depth);

@@ -210,8 +210,8 @@ def test_concurrent_waits_on_one_ticket():
     eng.close()
 
 
-@pytest.mark.parametrize("queue", [0, 1])
-def test_pipelined_mirror_frames_against_the_oracle(queue):
+@pytest.mark.parametrize("queue,tail", [(0, 0), (1, 0), (1, 2)])
+def test_pipelined_mirror_frames_against_the_oracle(queue, tail):
     """Mirror frames in flight (each slot has its own bounce queues and counters): every frame
     equals the oracle and carries the oracle's secondary-ray count."""
     from test_gpu_features import _mirror_corridor
@@ -219,6 +219,7 @@ def test_pipelined_mirror_frames_against_the_oracle(queue):
     ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
     eng = M.RayTracerEngine(sc)
     eng.set_option("queue", queue)
+    eng.set_option("queue_tail", tail)
     Q = A.RT_MAX_IN_FLIGHT
     fbs = [M.pinned_array((56, 80, 4), np.uint8) for _ in range(Q)]
     pend = []

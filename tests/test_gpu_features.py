@@ -315,15 +315,16 @@ def _rough_mirror_scene(w=128, h=96):
     return sc
 
 
-@pytest.mark.parametrize("queue", [0, 1])
-def test_queued_bounces_against_the_oracle(queue):
+@pytest.mark.parametrize("queue,tail", [(0, 0), (1, 0), (1, 1), (1, 2)])
+def test_queued_bounces_against_the_oracle(queue, tail):
     """Mirror/conductor scenes through the compacted bounce render (option queue = 1, the default:
     primary pass + one k_bounce launch per level, rays resolved backward through their queue
-    records) and through the bounce megakernel (0): both equal the oracle's recursion
+    records; with queue_tail = t the levels >= t traced depth-first in one k_bounce_tail launch)
+    and through the bounce megakernel (0): all equal the oracle's recursion
     (Object+Extension.swift:189-206, 252-283).  Covers the general walk (a transformed
     instance), rough mirrors, spp 3 (one traced sample divided by 3), the unified walk with 15
     queue levels, chunk selections, and several replicas."""
-    opt = {"queue": queue}
+    opt = {"queue": queue, "queue_tail": tail}
     sc = _rough_mirror_scene()
     st = _compare(sc, options=opt)
     assert st.secondary_rays > 0
@@ -338,6 +339,7 @@ def test_queued_bounces_against_the_oracle(queue):
     ref, ref8, ost = oracle.OracleScene(sc).render(0, threads=0, rgba=True)
     eng = M.RayTracerEngine(sc, devices=[0, 0, 0])
     eng.set_option("queue", queue)
+    eng.set_option("queue_tail", tail)
     for _ in range(2):                                 # queue words must be back at zero
         rgb, rgba, st = eng.render_rows(0, 0, 1, True)
         assert float(np.abs(rgb - ref).max()) <= TOL and np.array_equal(rgba, ref8)

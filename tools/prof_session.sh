@@ -7,11 +7,12 @@ tag="$1"; shift
 B="python3 bench.py --steps 20 --warmup 3 --in-flight 1 --no-cpu-baseline --no-side-paths $*"
 # the frame's render kernel: <COUNT, BOUNCE, WALK (1 = identity, 2 = transformed), QUEUE>; C5 (mirror
 # scene, render option queue = 1) is a frame chain: the queued primary pass, then per level
-# k_bounce, then k_queue_done (tools/pmc_roofline.py sums it per frame)
+# k_bounce, the sparse last levels in one k_bounce_tail, then k_queue_done (tools/pmc_roofline.py sums
+# it per frame)
 KX=""
 case " $* " in
   *" --config c5 "*) K="${KERNEL:-render_kernel<false, false, 1, true>}"
-                     KX="--kernel 'k_bounce<1>' --kernel k_queue_done" ;;
+                     KX="--kernel 'k_bounce<1>' --kernel 'k_bounce_tail<1>' --kernel k_queue_done" ;;
   *" --config c3i "*) K="${KERNEL:-render_kernel<false, false, 3, false>}" ;;
   # full trace() frames (C3g / C3d: level passes; C3r: depth-first k_events): the frame chain
   *" --config c3g "*|*" --config c3d "*) K="${KERNEL:-k_level<1>}"
