@@ -2078,11 +2078,14 @@ static bool queue_arena(const rt_scene* s, DeviceReplica& r, BounceArena* arena,
     if (P.cam.n != 1 || P.max_depth < 1 || P.max_depth > kMaxQueueLevels) return false;
     const int64_t levels = P.max_depth;
     const int64_t worst = (tiles + kQRegions - 1) / kQRegions * 64;
+    // levels past k_bounce_tail's (option queue_tail) are traced in its lanes: no records
+    const int64_t tail = s->opt[kOptQueueTail];
+    const int64_t top = tail > 0 ? std::min(levels, tail) : levels;
     int64_t want[kMaxQueueLevels + 1] = {};
     bool grow = arena->base == nullptr || levels > arena->levels;
     for (int64_t L = 1; L <= levels; ++L) {
         const int64_t h = r.qhint[L];
-        want[L] = !arena->by_need ? worst : std::min(worst, h > 0 ? h + h / 4 + 64 : worst / 16 + 64);
+        want[L] = L > top ? 0 : !arena->by_need ? worst : std::min(worst, h > 0 ? h + h / 4 + 64 : worst / 16 + 64);
         grow = grow || arena->cap[L] < want[L];
     }
     if (grow) {
